@@ -1,0 +1,102 @@
+"""Synthetic 2-D LiDAR room scans (SURVEY.md §8d generator).
+
+The reference has no recorded data (its only data file, ``./data/scan_prop.txt``
+read by ``line_detection.py:29``, is not shipped), so every benchmark and test
+scan is synthetic.  One scan = one RPLidar revolution seen from a robot pose
+inside a 4000 x 3000 mm rectangular room:
+
+* pose: x, y uniform with an 800 mm margin, heading uniform on (-pi, pi];
+* ``n_beams`` beams at ``theta_k = k * 360 / n_beams`` degrees, RPLidar
+  convention (clockwise, 0 = forward), i.e. the angle that
+  ``functions.py:59-60`` feeds into ``d*cos(-theta*pi/180 + pi/2)``;
+* range = ray-to-wall distance + N(0, 5 mm), 3 % outliers uniform in
+  [150, 5000] mm, optional zero-range dropouts.
+
+Everything is seeded by ``np.random.default_rng(1_000_003 * scan_id + cfg)``
+so any shard of a batch can be regenerated independently on any rank.
+Pure NumPy; works under numpy 1.26 (fixture container) and 2.x.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ROOM_W = 4000.0
+ROOM_H = 3000.0
+MARGIN = 800.0
+NOISE_MM = 5.0
+OUTLIER_FRAC = 0.03
+CHUNK = 100  # functions.py:14 MIN_NEIGHBOORS
+
+
+def _ray_room(px, py, ang):
+    """Distance from (px, py) along direction ``ang`` (rad, CCW from +x) to the
+    walls of [0, W] x [0, H]."""
+    c = np.cos(ang)
+    s = np.sin(ang)
+    big = np.full_like(ang, np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tx = np.where(c > 1e-12, (ROOM_W - px) / c, np.where(c < -1e-12, (0.0 - px) / c, big))
+        ty = np.where(s > 1e-12, (ROOM_H - py) / s, np.where(s < -1e-12, (0.0 - py) / s, big))
+    return np.minimum(tx, ty)
+
+
+def scan_polar(scan_id: int, n_beams: int = 720, cfg: int = 0, dropout: float = 0.0):
+    """Return (theta_deg, dist_mm, pose) for one synthetic revolution."""
+    rng = np.random.default_rng(1_000_003 * int(scan_id) + int(cfg))
+    px = rng.uniform(MARGIN, ROOM_W - MARGIN)
+    py = rng.uniform(MARGIN, ROOM_H - MARGIN)
+    heading = -rng.uniform(-np.pi, np.pi)  # uniform on (-pi, pi]
+    theta = np.arange(n_beams, dtype=np.float64) * (360.0 / n_beams)
+    # beam direction in the world frame: robot heading + (pi/2 - theta_rad)
+    world = heading + (np.pi / 2 - np.deg2rad(theta))
+    dist = _ray_room(px, py, world) + rng.normal(0.0, NOISE_MM, n_beams)
+    out = rng.random(n_beams) < OUTLIER_FRAC
+    dist = np.where(out, rng.uniform(150.0, 5000.0, n_beams), dist)
+    if dropout > 0.0:
+        dist = np.where(rng.random(n_beams) < dropout, 0.0, dist)
+    return theta, dist, np.array([px, py, heading])
+
+
+def polar_to_xy_ref(theta_deg, dist):
+    """NumPy form of ``functions.py:59-60`` (x = d*cos(-theta*A + pi/2))."""
+    a = -np.asarray(theta_deg, dtype=np.float64) * (np.pi / 180) + np.pi / 2
+    d = np.asarray(dist, dtype=np.float64)
+    return np.stack([d * np.cos(a), d * np.sin(a)], axis=-1)
+
+
+def chunk_sizes(n_points: int, chunk: int = CHUNK):
+    """Chunk sizes ``functions.py:61-76`` emits for one revolution of
+    ``n_points`` measures: full chunks of ``chunk`` points, then the remainder
+    only if it holds more than 2 points (a remainder of 1-2 points is
+    dropped, ``functions.py:71-74``)."""
+    sizes = [chunk] * (n_points // chunk)
+    rem = n_points % chunk
+    if rem > 2:
+        sizes.append(rem)
+    return sizes
+
+
+def make_batch(scan_ids, n_beams: int = 720, cfg: int = 0):
+    """Cartesian batch in the drop-in layout.
+
+    Returns dict with ``xy`` (P,2) f64 (AoS, points of dropped remainders
+    excluded), ``scan_chunk_off`` (S+1) i32, ``chunk_pt_off`` (C+1) i32,
+    ``poses`` (S,3).
+    """
+    xs, poses, sco, cpo = [], [], [0], [0]
+    for s in scan_ids:
+        th, d, pose = scan_polar(s, n_beams, cfg)
+        xy = polar_to_xy_ref(th, d)
+        sizes = chunk_sizes(n_beams)
+        used = int(sum(sizes))
+        xs.append(xy[:used])
+        for n in sizes:
+            cpo.append(cpo[-1] + n)
+        sco.append(sco[-1] + len(sizes))
+        poses.append(pose)
+    return {
+        "xy": np.ascontiguousarray(np.concatenate(xs, axis=0)),
+        "scan_chunk_off": np.asarray(sco, dtype=np.int32),
+        "chunk_pt_off": np.asarray(cpo, dtype=np.int32),
+        "poses": np.asarray(poses),
+    }
