@@ -1,0 +1,266 @@
+"""Benchmark: scans/s of the fused RANSAC + landmark + UKF hot path (BASELINE.json).
+
+python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1: launched by the driver as
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+         --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (config C3 of BASELINE.json, per GPU): 4096 synthetic 720-point scans
+(SURVEY §8d generator), chunked 7x100 + 20 as functions.py:64-76 does; per
+chunk skimage-semantics RANSAC (100 trials, 20 mm, numpy legacy MT19937 stream
+seeded per scan: results identical to the reference), landmark association
+(ransac_functions.py:34-54), then one UKF predict+update per scan with
+L = 20 landmarks (dim_z = 40).  One step = one pass over the batch = one launch
+of lslam_scan_pipeline.  Inputs are resident in HBM before timing.  Multi-GPU:
+each rank owns its own 4096 scans (ids rank*4096 ...), no data-path
+collective; torch.distributed (gloo) is used only for the barrier and the
+max-over-ranks of the elapsed time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec); the RANSAC residuals are FP64 VALU work
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FLOPS_PER_EVAL = 12       # residual + inlier test per (point, hypothesis): SURVEY §8d
+
+
+def make_workload(scan_ids, n_beams, L, seed_base=0):
+    from lidar_slam_amd import synth
+    from oracle import ukf as oukf  # noqa: F401  (only for the data generator's hx below)
+    b = synth.make_batch(scan_ids, n_beams)
+    S = len(scan_ids)
+    rng = np.random.default_rng(424242 + seed_base)
+    poses = b["poses"]
+    lmk = rng.uniform(-3000.0, 3000.0, (S, L, 2))
+    dx = lmk[:, :, 0] - poses[:, None, 0]
+    dy = lmk[:, :, 1] - poses[:, None, 1]
+    d = np.sqrt(dx * dx + dy * dy) + rng.normal(0, 0.5, (S, L))
+    ph = np.arctan2(dy, dx) - poses[:, None, 2] + rng.normal(0, 0.3, (S, L))
+    ph = (ph + np.pi) % (2 * np.pi) - np.pi
+    z = np.stack([d, ph], -1).reshape(S, 2 * L)
+    ukf = dict(n_landmarks=L, x=poses.copy(), P=np.tile(np.diag([.1, .1, .05]), (S, 1, 1)),
+               u=np.tile([2.0, 2.5], (S, 1)), z=z, lmk=lmk, R_diag=np.array([0.25, 0.09] * L))
+    return b, ukf
+
+
+def _twin_worker(args):
+    xy, cpo, seed, ukf_in = args
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    from oracle import numpy_twin as tw
+    from oracle import ukf as oukf
+    tw.process_scan(xy, cpo, seed)
+    x, P, u, z, lmk, Rd = ukf_in
+    oukf.ukf_batch(x[None], P[None], u[None], z[None], lmk[None], Rd)
+    return 1
+
+
+def cpu_baseline(n_scans, n_beams, L, procs):
+    """The reference's CPU path (NumPy twin, per-trial skimage structure) +
+    the NumPy UKF restatement, over a bounded sample, on `procs` host cores."""
+    import multiprocessing as mp
+    ids = list(range(n_scans))
+    b, ukf = make_workload(ids, n_beams, L)
+    sco, cpo = b["scan_chunk_off"], b["chunk_pt_off"]
+    jobs = []
+    for s in ids:
+        c0, c1 = sco[s], sco[s + 1]
+        jobs.append((b["xy"][cpo[c0]:cpo[c1]], cpo[c0:c1 + 1] - cpo[c0], s,
+                     (ukf["x"][s], ukf["P"][s], ukf["u"][s], ukf["z"][s], ukf["lmk"][s], ukf["R_diag"])))
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        pool.map(_twin_worker, jobs[:procs])  # warm the workers (imports)
+        t0 = time.perf_counter()
+        done = sum(pool.map(_twin_worker, jobs, chunksize=max(1, len(jobs) // (4 * procs))))
+        dt = time.perf_counter() - t0
+    return done / dt, dt
+
+
+def load_traffic(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scans", type=int, default=4096, help="scans per GPU")
+    ap.add_argument("--beams", type=int, default=720)
+    ap.add_argument("--landmarks", type=int, default=20)
+    ap.add_argument("--trials", type=int, default=100)
+    ap.add_argument("--hyp", default="mt19937", choices=["mt19937", "philox"])
+    ap.add_argument("--no-ukf", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=384)
+    ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--also-philox", action="store_true", help="also time the Philox (throughput) mode")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    L = args.landmarks
+
+    # CPU baseline first: before anything touches the GPU (the pool forks)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        procs = args.cpu_procs or max(1, min(16, os.cpu_count() or 1))
+        rate, dt = cpu_baseline(args.cpu_sample, args.beams, L, procs)
+        cpu = {"value": round(rate, 2), "unit": "scans/s", "cores": procs, "kind": "port",
+               "sample": "%d synthetic %d-pt scans (same generator, per-scan seeds) through the NumPy twin of "
+                         "the reference (skimage-structured ransac + landmark association, oracle/numpy_twin.py) "
+                         "+ the NumPy UKF restatement (oracle/ukf.py), %d processes, %.1f s wall"
+                         % (args.cpu_sample, args.beams, procs, dt)}
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from lidar_slam_amd import _lib
+    from lidar_slam_amd.device import Context
+    from lidar_slam_amd.pipeline import ScanPipeline
+
+    ctx = Context(local)
+    S = args.scans
+    ids = list(range(rank * S, (rank + 1) * S))
+    b, ukf = make_workload(ids, args.beams, L, seed_base=rank)
+    pipe = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
+                        max_trials=args.trials, hyp=args.hyp, lmk_capacity=32, want_yproj=True,
+                        ukf=None if args.no_ukf else ukf)
+    try:
+        import torch
+        have_torch_cuda = torch.cuda.is_available()
+        if have_torch_cuda:
+            torch.cuda.set_device(local)
+    except Exception:
+        torch, have_torch_cuda = None, False
+
+    def sync_all():
+        ctx.sync()
+        if have_torch_cuda:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        pipe.run(sync=False)
+    sync_all()
+    ctx.set_timing(True)
+    ctx.timing_reset()
+    barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.run(sync=False)
+    sync_all()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kms, klaunch = ctx.timing(_lib.K_PIPELINE)
+    ctx.set_timing(False)
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kms / max(klaunch, 1)], dtype=torch.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kavg = float(k.item())
+    else:
+        kavg = kms / max(klaunch, 1)
+
+    # sanity: results are well-formed (every chunk fitted or flagged)
+    r = pipe.results()
+    valid = int(np.sum((r["models"]["flags"] & 1) != 0))
+
+    total_scans = S * world * args.steps
+    value = total_scans / elapsed
+    evals = int(np.sum(np.diff(b["chunk_pt_off"])) * args.trials)   # (point, hypothesis) pairs per step
+    flops = FLOPS_PER_EVAL * evals
+    achieved_tf = flops / (kavg * 1e-3) / 1e12
+    n_pts = int(b["chunk_pt_off"][-1])
+    n_chunks = int(b["scan_chunk_off"][-1])
+    # algorithmic HBM bytes per launch: points in (16 B), mask (1 B) + projected y (8 B) out, chunk CSR
+    # (4 B) + model record (112 B) per chunk, per scan: seed, CSR, landmark count in/out + the list written
+    alg_bytes = n_pts * (16 + 1 + 8) + n_chunks * (4 + 112) + S * (4 + 4 + 8) + int(np.sum(r["lmk_count"])) * 56
+    if not args.no_ukf:
+        alg_bytes += S * (3 * 8 * 2 + 9 * 8 * 2 + 2 * 8 + 2 * L * 8 + 2 * L * 8)
+    hbm_gbs = alg_bytes / (kavg * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic)
+    traffic_bytes = None
+    if traffic and traffic.get("scans") == S and traffic.get("hyp") == args.hyp:
+        traffic_bytes = traffic.get("bytes_per_launch")
+
+    out = {
+        "metric": "scans/sec (RANSAC+UKF, 720-pt scans) at 1/2/4/8 MI355X + HBM GB/s vs peak",
+        "value": round(value, 1),
+        "unit": "scans/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY 8d room-scan generator; per-scan seeds)",
+        "config": {
+            "workload": "C3: %d synthetic %d-pt scans per GPU, chunked 7x100+20; RANSAC (%d trials, 20 mm, %s "
+                        "hypotheses) + landmark association + UKF predict/update (n=3, L=%d)%s"
+                        % (S, args.beams, args.trials, args.hyp, L, " [UKF off]" if args.no_ukf else ""),
+            "scans_per_gpu": S, "points_per_scan": args.beams, "trials": args.trials, "landmarks": L,
+            "hyp": args.hyp, "parallelism": "dp%d (scan shards, no collective)" % world,
+        },
+        "roofline": {
+            "bound": "fp64-valu",
+            "achieved": round(achieved_tf, 4),
+            "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5),
+            "traffic": traffic_bytes,
+            "kernel": "scan_kernel (lslam_scan_pipeline)",
+            "kernel_ms": round(kavg, 4),
+            "flops_per_launch": flops,
+            "alg_bytes_per_launch": alg_bytes,
+            "hbm_alg_gbs": round(hbm_gbs, 2),
+            "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 5),
+        },
+        "cpu_baseline": cpu,
+        "valid_chunks": valid,
+    }
+    if args.also_philox and world == 1:
+        pipe2 = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], max_trials=args.trials,
+                             hyp="philox", lmk_capacity=32, ukf=None if args.no_ukf else ukf)
+        for _ in range(args.warmup):
+            pipe2.run(sync=False)
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pipe2.run(sync=False)
+        ctx.sync()
+        out["philox_scans_per_s"] = round(S * args.steps / (time.perf_counter() - t0), 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+/*
+ * lidarslam.h — C ABI of the MI355X-native per-scan hot path of
+ * Farofeiro231/LiDAR_SLAM (RANSAC line/landmark extraction + UKF step).
+ *
+ * Plain pointers and sizes only; no torch, no C++ types.  Every function
+ * returns an int status (LSLAM_OK = 0, < 0 on error) and never aborts.
+ * Device pointers are HIP device memory (lslam_malloc or any hipMalloc'd
+ * buffer); work is enqueued on the context's own HIP stream and is
+ * asynchronous unless stated otherwise (lslam_sync waits).
+ *
+ * Reference interfaces each entry point replaces (reference = /root/reference,
+ * fit.py = scikit-image 0.18.3 skimage/measure/fit.py, the third-party code the
+ * reference calls):
+ *   lslam_polar_to_xy     functions.py:59-60   (dX, dY of each measure)
+ *   lslam_hyp_mt19937     fit.py:819-826 random_state.choice(N, 2, replace=False)
+ *                         on the global np.random legacy MT19937 stream
+ *   lslam_ransac          ransac_functions.py:23-31  ransac(data, LineModelND, 2, 20,
+ *                         max_trials=100) + a, b, tip (fit.py:581-881, 19-132)
+ *   lslam_landmarks       ransac_functions.py:34-54 association walk +
+ *                         landmarking.py:48-77 + check_ransac append (:75-76)
+ *   lslam_scan_pipeline   ransac_functions.py:63-93 check_ransac over the chunks
+ *                         of many scans (landmark_extraction per chunk), fused with
+ *                         the UKF step below
+ *   lslam_ukf_step        systemClass.py:12-29 System.ukf.predict(u=..) +
+ *                         .update(z, landmarks=..) with UKFMethods.py:10-71
+ *                         callbacks (filterpy 1.4.5 UnscentedKalmanFilter semantics)
+ */
+#ifndef LIDARSLAM_H
+#define LIDARSLAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSLAM_ABI_VERSION 1
+
+/* ---- status codes ---- */
+enum {
+    LSLAM_OK = 0,
+    LSLAM_ERR_ARG = -1,         /* invalid argument (ValueError in the reference) */
+    LSLAM_ERR_HIP = -2,         /* HIP runtime error (message: lslam_last_error) */
+    LSLAM_ERR_NOMEM = -3,
+    LSLAM_ERR_CAPACITY = -4,    /* a landmark list or chunk count exceeded its capacity */
+    LSLAM_ERR_UNSUPPORTED = -5  /* e.g. min_samples != 2 */
+};
+
+/* ---- per-chunk flags (lslam_chunk_model.flags) ---- */
+enum {
+    LSLAM_VALID = 1,          /* model fitted; landmark_extraction returned normally */
+    LSLAM_N_TOO_SMALL = 2,    /* N < 3: fit.py:798-799 ValueError, no RNG consumed */
+    LSLAM_NO_INLIERS = 4,     /* fit.py:877-879 (None, None) -> AttributeError at ransac_functions.py:25 */
+    LSLAM_EST_FAIL = 8,       /* 1 final inlier: fit.py:96-97 ValueError */
+    LSLAM_EARLY_STOP = 16,    /* stop_residuals_sum hit (sum of squared residuals == 0) */
+    LSLAM_VERTICAL = 32,      /* final direction x == 0: a = +-inf/nan (ransac_functions.py:26) */
+    LSLAM_NEW_LANDMARK = 64,  /* no landmark matched: the chunk's Landmark was appended */
+    LSLAM_MATCHED = 128       /* an existing landmark matched (its life reset to LIFE) */
+};
+
+/* ---- hypothesis sources ---- */
+enum {
+    LSLAM_HYP_MT19937 = 0,  /* numpy legacy RandomState stream, bit-exact with the reference */
+    LSLAM_HYP_PHILOX = 1,   /* counter-based Philox4x32-10, statistically equivalent only */
+    LSLAM_HYP_EXPLICIT = 2  /* caller-provided draws (lslam_scan_batch.hyp) */
+};
+
+/* ---- UKF flags ---- */
+enum {
+    LSLAM_UKF_PREDICT = 1,
+    LSLAM_UKF_UPDATE = 2,
+    LSLAM_UKF_LMK_FROM_RANSAC = 4  /* landmark slot c <- chunk c's Landmark.pos (fused pipeline) */
+};
+
+/* One RANSAC call's result (one chunk), 112 bytes. */
+typedef struct lslam_chunk_model {
+    double ox, oy;          /* final model origin   (model_robust.params[0]) */
+    double ux, uy;          /* final model direction (params[1]; sign arbitrary) */
+    double a, b;            /* y = a*x + b         (ransac_functions.py:26-27) */
+    double tip_x, tip_y;    /* Landmark.end        (ransac_functions.py:29-30) */
+    double proj_a, proj_b;  /* line used for yBase: matched landmark's or own (:46,:49,:53) */
+    int32_t n_inliers;      /* popcount of the inlier mask */
+    int32_t best_trial;     /* winning hypothesis index (-1 if none) */
+    int32_t n_draws;        /* choice() draws consumed: T+1, or stop_trial+2 on early stop */
+    int32_t flags;          /* LSLAM_* flags above */
+    int32_t match_index;    /* index of the matched landmark in the pre-call list, -1 if none */
+    int32_t landmark_id;    /* landmarkNumber given to this chunk's Landmark */
+    int32_t n_points;       /* chunk size N */
+    int32_t reserved;
+} lslam_chunk_model;
+
+/* landmarking.Landmark (landmarking.py:12-19), 56 bytes. */
+typedef struct lslam_landmark {
+    double a, b;
+    double pos_x, pos_y;   /* Landmark.pos = final model origin */
+    double end_x, end_y;   /* Landmark.end = (tipX, tipY) */
+    int32_t id;
+    int32_t life;
+} lslam_landmark;
+
+typedef struct lslam_ransac_params {
+    double residual_threshold;  /* ransac_functions.py:9  THRESHOLD = 20 */
+    int32_t max_trials;         /* ransac_functions.py:10 MAX_TRIALS = 100 */
+    int32_t min_samples;        /* ransac_functions.py:11 MIN_SAMPLES = 2 (only 2 supported) */
+    int32_t hyp_source;         /* LSLAM_HYP_* */
+    int32_t life;               /* landmarking.py:3 LIFE = 40 */
+    double tol_a;               /* landmarking.py:4 TOLERANCE_A = 0.1 */
+    double tol_b;               /* landmarking.py:5 TOLERANCE_B = 10 */
+    double tol_dist;            /* landmarking.py:6 TOLERANCE = 100 */
+    uint64_t philox_seed;       /* LSLAM_HYP_PHILOX key */
+} lslam_ransac_params;
+
+typedef struct lslam_ukf_params {
+    int32_t n_landmarks;     /* L; dim_z = 2L (systemClass.py:7 LANDMARK_NUMBER = 8) */
+    int32_t flags;           /* LSLAM_UKF_* */
+    double dt;               /* systemClass.py:10 DT = 0.005 */
+    double wheel_radius;     /* UKFMethods.py:6 R = 50 (mm) */
+    double wheel_base;       /* UKFMethods.py:7 L = 200 (mm) */
+    double alpha, beta, kappa; /* systemClass.py:20 MerweScaledSigmaPoints(3, 1e-4, 2, 0) */
+    double Q[9];             /* systemClass.py:29 Q = 1e-3 * I3 */
+} lslam_ukf_params;
+
+/* A batch of scans, all pointers DEVICE memory (NULL = absent where optional). */
+typedef struct lslam_scan_batch {
+    int32_t n_scans;
+    int32_t n_chunks;               /* = scan_chunk_off[n_scans] */
+    int64_t n_points;               /* = chunk_pt_off[n_chunks] */
+    int32_t max_chunk_points;       /* max chunk size N over the batch */
+    int32_t max_scan_chunks;        /* max chunks per scan */
+    int32_t lmk_capacity;           /* per-scan landmark list capacity */
+    int32_t reserved;
+    /* inputs */
+    const double *xy;               /* [n_points][2] fp64 Cartesian points (AoS) */
+    const int32_t *scan_chunk_off;  /* [n_scans+1] CSR scan -> chunks */
+    const int32_t *chunk_pt_off;    /* [n_chunks+1] CSR chunk -> points */
+    const uint32_t *seeds;          /* [n_scans] np.random.seed(seed) per scan (MT19937 mode) */
+    const uint32_t *mt_state_in;    /* [n_scans][625] key[624] + pos, overrides seeds */
+    uint32_t *mt_state_out;         /* [n_scans][625] state after the scan (optional) */
+    const int32_t *hyp;             /* [n_chunks][max_trials+1][2] (LSLAM_HYP_EXPLICIT) */
+    const int32_t *id_base;         /* [n_scans] landmarkNumber of the first chunk (optional, 0) */
+    lslam_landmark *landmarks;      /* [n_scans][lmk_capacity] in/out (optional) */
+    int32_t *lmk_count;             /* [n_scans] in/out (required with landmarks) */
+    /* outputs */
+    uint8_t *inlier_mask;           /* [n_points] */
+    lslam_chunk_model *models;      /* [n_chunks] */
+    double *y_proj;                 /* [n_points] projected y of inliers, 0 elsewhere (optional) */
+    int32_t *draws_out;             /* [n_chunks][max_trials+1][2] (optional, parity/debug) */
+    int32_t *trial_cnt_out;         /* [n_chunks][max_trials] (optional, parity/debug) */
+    /* UKF, per scan */
+    double *ukf_x;                  /* [n_scans][3] in/out */
+    double *ukf_P;                  /* [n_scans][3][3] in/out */
+    const double *ukf_u;            /* [n_scans][2]  [vl, vr] */
+    const double *ukf_z;            /* [n_scans][2L] interleaved [d0, phi0, d1, phi1, ...] */
+    const double *ukf_lmk;          /* [n_scans][L][2] landmark positions */
+    const double *ukf_R_diag;       /* [2L] measurement noise diagonal (systemClass.py:28) */
+} lslam_scan_batch;
+
+typedef struct lslam_ctx lslam_ctx;  /* opaque: device, stream, events, scratch */
+
+/* ---- library / context ---- */
+const char *lslam_version(void);
+const char *lslam_status_string(int status);
+const char *lslam_last_error(void);  /* thread-local message of the last error */
+int lslam_device_count(int *n);
+int lslam_ctx_create(int device, lslam_ctx **out);
+int lslam_ctx_destroy(lslam_ctx *ctx);
+int lslam_sync(lslam_ctx *ctx);
+int lslam_malloc(lslam_ctx *ctx, size_t bytes, void **dptr);
+int lslam_free(lslam_ctx *ctx, void *dptr);
+int lslam_host_alloc(size_t bytes, void **hptr);  /* pinned host memory */
+int lslam_host_free(void *hptr);
+int lslam_h2d(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
+int lslam_d2h(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
+int lslam_memset(lslam_ctx *ctx, void *dst, int value, size_t bytes);     /* async */
+/* per-kernel HIP-event timing on the ctx stream (kernel ids: LSLAM_K_*) */
+enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMARK = 3, LSLAM_K_UKF = 4, LSLAM_K_COUNT = 5 };
+int lslam_set_timing(lslam_ctx *ctx, int enable);
+int lslam_timing(lslam_ctx *ctx, int kernel, double *total_ms, int64_t *launches);  /* syncs */
+int lslam_timing_reset(lslam_ctx *ctx);
+
+/* ---- host helpers ---- */
+int lslam_ransac_params_default(lslam_ransac_params *p);
+int lslam_ukf_params_default(lslam_ukf_params *p, int32_t n_landmarks);
+/* smallest e with RN(sqrt(e)) >= thr: (residual < thr) <=> (squared residual < cutoff) */
+double lslam_inlier_cutoff(double thr);
+/* MerweScaledSigmaPoints weights (filterpy _compute_weights) for n = 3 */
+int lslam_ukf_weights(const lslam_ukf_params *p, double *Wm7, double *Wc7, double *lambda_plus_n);
+/* numpy RandomState(seed) state: key[624] + pos (host memory, 625 words) */
+int lslam_mt_seed_state(uint32_t seed, uint32_t *state625);
+
+/* ---- hot path (device pointers, async on the ctx stream) ---- */
+/* A1: xy[i] = (d cos(-th*pi/180 + pi/2), d sin(...)); n measures */
+int lslam_polar_to_xy(lslam_ctx *ctx, const double *theta_deg, const double *dist, double *xy, int64_t n);
+/* A3: the draws each chunk's ransac would make, assuming no early stop
+ * (draws_out [n_chunks][max_trials+1][2]).  Uses b->seeds/mt_state_in/mt_state_out. */
+int lslam_hyp_mt19937(lslam_ctx *ctx, const lslam_scan_batch *b, int32_t max_trials);
+/* A3-A8: ransac per chunk (chained RNG per scan), masks, models */
+int lslam_ransac(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p);
+/* A9-A10: association over b->models (already fitted) + y_proj */
+int lslam_landmarks(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p);
+/* U1-U8: one predict and/or update per scan */
+int lslam_ukf_step(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ukf_params *u);
+/* A3-A10 (+ U1-U8 if u != NULL) fused: one wave per scan, one launch */
+int lslam_scan_pipeline(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p,
+                        const lslam_ukf_params *u);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIDARSLAM_H */

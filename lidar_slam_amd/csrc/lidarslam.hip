@@ -1,0 +1,1080 @@
+// lidarslam.hip — MI355X (gfx950) kernels + C ABI for the per-scan hot path of
+// Farofeiro231/LiDAR_SLAM.  See include/lidarslam.h for the reference entry
+// points each function replaces and DESIGN.md for the layout/roofline notes.
+//
+// Execution model: ONE wave (64 lanes) per scan, one scan per workgroup,
+// grid = n_scans.  Inside a scan the chunks are processed in order (the legacy
+// RNG stream is chained across them, ransac_functions.py:73 + fit.py:791):
+//   A3 draws -> A4/A5 counts (lane = hypothesis) -> A6 tie sums + selection
+//   -> mask + A7 refit -> A8 line params -> A9/A10 association -> (U1-U8 UKF)
+// Everything a scan touches lives in LDS/registers; HBM sees the points once
+// (16 B/point) and the outputs once.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared.
+// -ffp-contract=off is REQUIRED: hipcc contracts a*b+c into v_fma_f64 by
+// default, which would change the reference's rounding.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <atomic>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "../../include/lidarslam.h"
+#include "lslam_rng.h"
+#include "lslam_ransac.h"
+#include "lslam_ukf.h"
+#include "lslam_wave.h"
+
+using namespace lslam;
+
+static_assert(sizeof(lslam_chunk_model) == 112, "chunk model ABI");
+static_assert(sizeof(lslam_landmark) == 56, "landmark ABI");
+
+enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8 };
+enum { LSLAM_CAPACITY_FLAG = 256 };
+
+// ------------------------------------------------------------------------
+// kernel arguments (passed by value)
+// ------------------------------------------------------------------------
+struct KArgs {
+    lslam_scan_batch b;
+    double ecut;
+    double thr;
+    double tol_a, tol_b, tol_dist;
+    uint64_t philox_seed;
+    int T;
+    int hyp_source;
+    int life;
+    // LDS layout (byte offsets into dynamic shared memory)
+    int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum, off_inl;
+    int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg;
+    int corg_cap;
+    int off_ukf;
+    uint32_t ring_mask;
+    int pts_cap;
+    int lmk_cap;
+    int hist_cap;
+    UkfConst ukf;
+};
+
+// ------------------------------------------------------------------------
+// per-chunk RANSAC on one wave
+// ------------------------------------------------------------------------
+struct ChunkOut {
+    Model m;          // final model (valid if flags & VALID)
+    int n_inl;
+    int last_inl;
+    int best;
+    int n_draws;
+    int flags;
+    int stop;         // trial at which the stop criterion fired, -1 if none
+};
+
+// counts for T trials over N points; returns M = max count
+__device__ __forceinline__ int count_pass(const double2 *P, int N, const int32_t *draws, int32_t *cnt, int T,
+                                          double ecut, int lane) {
+    int M = 0;
+    for (int tb = 0; tb < T; tb += 64) {
+        const int t = tb + lane;
+        const int tt = t < T ? t : 0;
+        const Model m = model2(P[draws[2 * tt]], P[draws[2 * tt + 1]]);
+        int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        int p = 0;
+        for (; p + 4 <= N; p += 4) {
+            const double2 q0 = P[p], q1 = P[p + 1], q2 = P[p + 2], q3 = P[p + 3];
+            c0 += resid2(q0, m) < ecut;
+            c1 += resid2(q1, m) < ecut;
+            c2 += resid2(q2, m) < ecut;
+            c3 += resid2(q3, m) < ecut;
+        }
+        for (; p < N; p++) c0 += resid2(P[p], m) < ecut;
+        const int c = (c0 + c1) + (c2 + c3);
+        if (t < T) cnt[t] = c;
+        M = max(M, wave_max(t < T ? c : 0));
+    }
+    __syncthreads();
+    return M;
+}
+
+// The whole ransac() call for one chunk whose draws are in LDS `draws`.
+__device__ ChunkOut chunk_ransac(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *cnt,
+                                 int32_t *tied, double *tsum, int32_t *inl, double *vstack, int *nstack,
+                                 int32_t *cnt_out, int lane) {
+    ChunkOut o;
+    o.flags = 0;
+    o.best = -1;
+    o.stop = -1;
+    o.n_inl = 0;
+    o.last_inl = -1;
+    o.n_draws = a.T + 1;
+    const int T = a.T;
+    const double ecut = a.ecut;
+    const int M = uni(count_pass(P, N, draws, cnt, T, ecut, lane));
+    if (cnt_out)
+        for (int t = lane; t < T; t += 64) cnt_out[t] = cnt[t];
+    // compact the max-count trials in trial order
+    int ntied = 0;
+    for (int tb = 0; tb < T; tb += 64) {
+        const int t = tb + lane;
+        const bool h = t < T && cnt[t] == M;
+        const uint64_t bm = ballot(h);
+        if (h) tied[ntied + (int)mbcnt(bm)] = t;
+        ntied += popc64(bm);
+    }
+    __syncthreads();
+    // tie sums: only needed if they can change the outcome or trigger the stop
+    const bool need_sums = ntied > 1 || M == N || !(ecut > 0.0);
+    if (need_sums) {
+        for (int kb = 0; kb < ntied; kb += 64) {
+            const int k = kb + lane;
+            const int t = tied[k < ntied ? k : 0];
+            const Model m = model2(P[draws[2 * t]], P[draws[2 * t + 1]]);
+            const double s = pw_sum(P, N, m, vstack, nstack, lane);
+            if (k < ntied) tsum[k] = s;
+        }
+        __syncthreads();
+    }
+    // sequential selection over the tied trials (fit.py:850-869)
+    int bcnt = 0, best = -1;
+    double bsum = __builtin_inf();
+    if (T > 0) {
+        if (!need_sums) {
+            best = tied[0];
+            bcnt = M;
+        } else {
+            for (int k = 0; k < ntied; k++) {
+                const int t = uni(tied[k]);
+                const double s = unid(tsum[k]);
+                if (M > bcnt || (M == bcnt && s < bsum)) {
+                    best = t;
+                    bcnt = M;
+                    bsum = s;
+                    if (bsum <= 0.0) {
+                        o.stop = t;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    best = uni(best);
+    o.best = best;
+    __syncthreads();  // tsum (read above) and inl (written below) share LDS
+    if (o.stop >= 0) {
+        o.n_draws = o.stop + 2;
+        o.flags |= LSLAM_EARLY_STOP;
+    }
+    if (best < 0) {
+        o.flags |= LSLAM_NO_INLIERS;
+        return o;
+    }
+    // inlier mask of the winner + inlier index list (data order)
+    const Model mw = model2(P[draws[2 * best]], P[draws[2 * best + 1]]);
+    int nin = 0, last = -1;
+    for (int pb = 0; pb < N; pb += 64) {
+        const int p = pb + lane;
+        const bool h = p < N && resid2(P[p < N ? p : 0], mw) < ecut;
+        const uint64_t bm = ballot(h);
+        if (h) inl[nin + (int)mbcnt(bm)] = p;
+        if (bm) last = pb + fls64(bm);
+        nin += popc64(bm);
+    }
+    __syncthreads();
+    o.n_inl = nin;
+    o.last_inl = last;
+    if (nin == 0) {
+        o.flags |= LSLAM_NO_INLIERS;
+        return o;
+    }
+    if (nin == 1) {
+        o.flags |= LSLAM_EST_FAIL;
+        return o;
+    }
+    Model f;
+    if (nin == 2) {
+        f = model2(P[inl[0]], P[inl[1]]);
+    } else {
+        // data.mean(axis=0): sequential add.reduce, then / n  (all lanes, same order)
+        double sx = 0.0, sy = 0.0;
+        {
+            const double2 q = P[inl[0]];
+            sx = q.x;
+            sy = q.y;
+        }
+        int i = 1;
+        for (; i + 4 <= nin; i += 4) {
+            const double2 q0 = P[inl[i]], q1 = P[inl[i + 1]], q2 = P[inl[i + 2]], q3 = P[inl[i + 3]];
+            sx += q0.x; sy += q0.y;
+            sx += q1.x; sy += q1.y;
+            sx += q2.x; sy += q2.y;
+            sx += q3.x; sy += q3.y;
+        }
+        for (; i < nin; i++) {
+            const double2 q = P[inl[i]];
+            sx += q.x;
+            sy += q.y;
+        }
+        f.ox = sx / (double)nin;
+        f.oy = sy / (double)nin;
+        double sxx = 0.0, sxy = 0.0, syy = 0.0;
+        for (int k = 0; k < nin; k++) {
+            const double2 q = P[inl[k]];
+            const double cx = q.x - f.ox, cy = q.y - f.oy;
+            sxx += cx * cx;
+            sxy += cx * cy;
+            syy += cy * cy;
+        }
+        tls_direction(sxx, sxy, syy, f.ux, f.uy);
+    }
+    o.m = f;
+    o.flags |= LSLAM_VALID;
+    if (f.ux == 0.0) o.flags |= LSLAM_VERTICAL;
+    return o;
+}
+
+// ------------------------------------------------------------------------
+// landmark association (ransac_functions.py:34-54, landmarking.py:48-77)
+// list in LDS: lmk[0..L)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ bool is_equal(const lslam_landmark &Lk, double a, double b, double px, double py,
+                                         double ex, double ey, const KArgs &ka) {
+    const double distA = fabs(Lk.a - a);
+    const double distB = fabs(Lk.b - b);
+    const double vx = Lk.end_x - px, vy = Lk.end_y - py;
+    const double dEO = cr_sqrt(__builtin_fma(vy, vy, vx * vx));
+    const double wx = Lk.pos_x - ex, wy = Lk.pos_y - ey;
+    const double dOE = cr_sqrt(__builtin_fma(wy, wy, wx * wx));
+    if (distA <= ka.tol_a && distB <= ka.tol_b) return (dEO <= ka.tol_dist || dOE <= ka.tol_dist);
+    return false;
+}
+
+// returns match index (pre-call) or -1; updates list + count; proj line out
+__device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, int &L, double a, double b,
+                         double px, double py, double ex, double ey, int id, double &pa, double &pb,
+                         bool &overflow, int lane) {
+    const int nblk = (L + 63) >> 6;
+    for (int i = lane; i < nblk; i += 64) vis[i] = 0ull;
+    __syncthreads();
+    int match = -1;
+    int k = 0;
+    // walk (ransac_functions.py:35-43) over pre-call indices: examine k; equal ->
+    // stop; else decrease_life; if it died it is removed and `i += 1` then skips
+    // the element that slid into its slot, i.e. pre-call index k+1.
+    for (int blk = 0; blk < nblk && match < 0 && k < L; blk++) {
+        if (k >= blk * 64 + 64) continue;
+        const int j = blk * 64 + lane;
+        bool eq = false, dies = false;
+        if (j < L) {
+            eq = is_equal(lmk[j], a, b, px, py, ex, ey, ka);
+            dies = lmk[j].life <= 1;
+        }
+        const uint64_t E = ballot(eq);
+        const uint64_t D = ballot(dies);
+        uint64_t V = 0;
+        const int hi = min(L, blk * 64 + 64);
+        while (k < hi) {
+            const int bit = k - blk * 64;
+            if ((E >> bit) & 1ull) {
+                match = k;
+                break;
+            }
+            V |= 1ull << bit;
+            k += ((D >> bit) & 1ull) ? 2 : 1;
+        }
+        if (lane == 0) vis[blk] = V;
+        __syncthreads();
+    }
+    pa = a;
+    pb = b;
+    if (match >= 0) {
+        pa = unid(lmk[match].a);
+        pb = unid(lmk[match].b);
+    }
+    // apply decrease_life / removal / reset_life, then compact in list order
+    int w = 0;
+    for (int blk = 0; blk < nblk; blk++) {
+        const int j = blk * 64 + lane;
+        const uint64_t V = vis[blk];
+        lslam_landmark e;
+        bool keep = false;
+        if (j < L) {
+            e = lmk[j];
+            if ((V >> lane) & 1ull) {
+                if (e.life > 0) e.life -= 1;
+                keep = e.life != 0;
+            } else {
+                keep = true;
+            }
+            if (j == match) e.life = ka.life;
+        }
+        const uint64_t km = ballot(keep);
+        __syncthreads();
+        if (keep) lmk[w + (int)mbcnt(km)] = e;
+        w += popc64(km);
+        __syncthreads();
+    }
+    L = w;
+    overflow = false;
+    if (match < 0) {
+        if (L < ka.lmk_cap) {
+            if (lane == 0) {
+                lslam_landmark F;
+                F.a = a; F.b = b; F.pos_x = px; F.pos_y = py; F.end_x = ex; F.end_y = ey;
+                F.id = id; F.life = ka.life;
+                lmk[L] = F;
+            }
+            L += 1;
+        } else {
+            overflow = true;
+        }
+    }
+    __syncthreads();
+    return match;
+}
+
+// ------------------------------------------------------------------------
+// the scan kernel
+// ------------------------------------------------------------------------
+template <int HYP, int MODE>
+__global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int s = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+
+    double2 *P = (double2 *)(smem + a.off_pts);
+    uint32_t *key = (uint32_t *)(smem + a.off_key);
+    int32_t *draws = (int32_t *)(smem + a.off_draws);
+    int32_t *cnt = (int32_t *)(smem + a.off_cnt);
+    int32_t *tied = (int32_t *)(smem + a.off_tied);
+    double *tsum = (double *)(smem + a.off_tsum);
+    int32_t *inl = (int32_t *)(smem + a.off_inl);
+    uint8_t *mk = (uint8_t *)(smem + a.off_mask);
+    double *vstack = (double *)(smem + a.off_vstack);
+    int *nstack = (int *)(smem + a.off_nstack);
+    int32_t *hist = (int32_t *)(smem + a.off_hist);
+    double2 *corg = (double2 *)(smem + a.off_corg);
+    lslam_landmark *lmk = (lslam_landmark *)(smem + a.off_lmk);
+    uint64_t *vis = (uint64_t *)(smem + a.off_vis);
+
+    const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
+    const int nchunks = c1 - c0;
+    const int T = a.T;
+
+    MTWave mt;
+    mt.key = key;
+    mt.ring = (uint16_t *)(smem + a.off_ring);
+    mt.ring_mask = a.ring_mask;
+    mt.pos = MT_N;
+
+    auto mt_init = [&]() {
+        if (B.mt_state_in) {
+            const uint32_t *src = B.mt_state_in + (size_t)s * 625;
+            for (int i = lane; i < MT_N; i += 64) key[i] = src[i];
+            mt.pos = uni((int)src[624]);
+            __syncthreads();
+        } else {
+            mt_seed(key, B.seeds ? B.seeds[s] : 0u, lane);
+            mt.pos = MT_N;
+        }
+    };
+
+    constexpr bool kRansac = (MODE & (MODE_RANSAC | MODE_HYP_ONLY)) != 0;
+    constexpr bool use_mt = kRansac && HYP == LSLAM_HYP_MT19937;
+    if (use_mt) mt_init();
+
+    // landmark list of this scan -> LDS
+    int L = 0;
+    if (MODE & MODE_ASSOC) {
+        if (B.landmarks) {
+            L = uni(B.lmk_count[s]);
+            if (L > a.lmk_cap) L = a.lmk_cap;
+            const lslam_landmark *src = B.landmarks + (size_t)s * a.lmk_cap;
+            for (int i = lane; i < L; i += 64) lmk[i] = src[i];
+        }
+        __syncthreads();
+    }
+    const int id0 = B.id_base ? B.id_base[s] : 0;
+
+    for (int ci = 0; ci < nchunks && (kRansac || (MODE & MODE_ASSOC)); ci++) {
+        const int c = c0 + ci;
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        lslam_chunk_model rec;
+        memset(&rec, 0, sizeof(rec));
+        rec.best_trial = -1;
+        rec.match_index = -1;
+        rec.landmark_id = id0 + ci;
+        rec.n_points = N;
+        bool have_model = false;
+        if (kRansac) {
+            if (ci < a.corg_cap && lane == 0) corg[ci] = make_double2(__builtin_nan(""), __builtin_nan(""));
+            if (N < 3) {
+                // fit.py:798-799: ValueError before any draw; nothing consumed
+                rec.flags = LSLAM_N_TOO_SMALL;
+                if (lane == 0 && B.models) B.models[c] = rec;
+                for (int p = lane; p < N; p += 64) {
+                    if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
+                    if (B.y_proj) B.y_proj[p0 + p] = 0.0;
+                }
+                if (use_mt && ci < a.hist_cap && lane == 0) hist[ci] = 0;
+                __syncthreads();
+                continue;
+            }
+            // ---- A3: draws
+            const int D = T + 1;
+            if (HYP == LSLAM_HYP_MT19937) {
+                mt_draws(mt, (uint32_t)N, (uint32_t)D, draws, true, lane);
+            } else if (HYP == LSLAM_HYP_PHILOX) {
+                philox_draws((uint32_t)N, (uint32_t)D, (uint32_t)c, a.philox_seed, draws, lane);
+            } else {
+                const int32_t *h = B.hyp + (size_t)c * 2 * D;
+                for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
+                __syncthreads();
+            }
+            if (B.draws_out) {
+                int32_t *dst = B.draws_out + (size_t)c * 2 * D;
+                for (int i = lane; i < 2 * D; i += 64) dst[i] = draws[i];
+            }
+            if (MODE & MODE_HYP_ONLY) {
+                if (use_mt && ci < a.hist_cap && lane == 0) hist[ci] = D;
+                __syncthreads();
+                continue;
+            }
+            // ---- stage the chunk's points in LDS (16 B per lane, coalesced)
+            const double2 *src = (const double2 *)B.xy + p0;
+            for (int p = lane; p < N; p += 64) P[p] = src[p];
+            __syncthreads();
+            // ---- A4-A7
+            const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack,
+                                            B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
+            if (use_mt) {
+                if (ci < a.hist_cap && lane == 0) hist[ci] = o.n_draws;
+                __syncthreads();
+                if (o.n_draws < D) {
+                    // early stop: rewind the stream to exactly o.n_draws draws into this chunk
+                    mt_init();
+                    for (int cj = 0; cj < ci && cj < a.hist_cap; cj++) {
+                        const int nj = B.chunk_pt_off[c0 + cj + 1] - B.chunk_pt_off[c0 + cj];
+                        const int dj = uni(hist[cj]);
+                        if (nj >= 3 && dj > 0) mt_draws(mt, (uint32_t)nj, (uint32_t)dj, nullptr, false, lane);
+                    }
+                    mt_draws(mt, (uint32_t)N, (uint32_t)o.n_draws, nullptr, false, lane);
+                }
+            }
+            // ---- mask (LDS copy + global)
+            const bool valid = (o.flags & LSLAM_VALID) != 0;
+            for (int p = lane; p < N; p += 64) mk[p] = 0;
+            __syncthreads();
+            if (valid)
+                for (int k = lane; k < o.n_inl; k += 64) mk[inl[k]] = 1;
+            __syncthreads();
+            if (B.inlier_mask)
+                for (int p = lane; p < N; p += 64) B.inlier_mask[p0 + p] = mk[p];
+            // ---- A8 line parameters (ransac_functions.py:25-31)
+            rec.n_inliers = valid ? o.n_inl : 0;
+            rec.best_trial = o.best;
+            rec.n_draws = o.n_draws;
+            rec.flags = o.flags;
+            if (valid) {
+                have_model = true;
+                const Model fm = o.m;
+                const double av = fm.uy / fm.ux;
+                const double bv = fm.oy - av * fm.ox;
+                const double tx = P[o.last_inl].x;
+                const double ty = tx * av + bv;
+                rec.ox = fm.ox; rec.oy = fm.oy; rec.ux = fm.ux; rec.uy = fm.uy;
+                rec.a = av; rec.b = bv; rec.tip_x = tx; rec.tip_y = ty;
+                rec.proj_a = av; rec.proj_b = bv;
+                if (ci < a.corg_cap && lane == 0) corg[ci] = make_double2(fm.ox, fm.oy);
+            }
+        } else {
+            // association-only mode: models and masks come from a previous ransac launch
+            rec = B.models[c];
+            have_model = (rec.flags & LSLAM_VALID) != 0;
+            for (int p = lane; p < N; p += 64) mk[p] = B.inlier_mask[p0 + p];
+            __syncthreads();
+        }
+
+        // ---- A9/A10 association + projection
+        if (MODE & MODE_ASSOC) {
+            if (have_model) {
+                double pa, pb;
+                bool overflow = false;
+                const int m = associate(a, lmk, vis, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
+                                        rec.landmark_id, pa, pb, overflow, lane);
+                rec.match_index = m;
+                rec.proj_a = pa;
+                rec.proj_b = pb;
+                rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
+                if (overflow) rec.flags |= LSLAM_CAPACITY_FLAG;
+            }
+        }
+        if (B.y_proj) {
+            const double pa = rec.proj_a, pb = rec.proj_b;
+            for (int p = lane; p < N; p += 64) {
+                const double x = B.xy[2 * (size_t)(p0 + p)];
+                B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
+            }
+        }
+        if (lane == 0 && B.models) B.models[c] = rec;
+        __syncthreads();
+    }
+
+    if (use_mt && B.mt_state_out) {
+        uint32_t *dst = B.mt_state_out + (size_t)s * 625;
+        for (int i = lane; i < MT_N; i += 64) dst[i] = key[i];
+        if (lane == 0) dst[624] = (uint32_t)mt.pos;
+    }
+    if ((MODE & MODE_ASSOC) && B.landmarks) {
+        lslam_landmark *dst = B.landmarks + (size_t)s * a.lmk_cap;
+        for (int i = lane; i < L; i += 64) dst[i] = lmk[i];
+        if (lane == 0) B.lmk_count[s] = L;
+    }
+
+    // ---- UKF step (U1-U8)
+    if (MODE & MODE_UKF) {
+        __syncthreads();
+        double x[3], Pm[9], u[2];
+        for (int i = 0; i < 3; i++) x[i] = B.ukf_x[3 * (size_t)s + i];
+        for (int i = 0; i < 9; i++) Pm[i] = B.ukf_P[9 * (size_t)s + i];
+        u[0] = B.ukf_u[2 * (size_t)s];
+        u[1] = B.ukf_u[2 * (size_t)s + 1];
+        const int Lu = a.ukf.L;
+        const double *lm = B.ukf_lmk + (size_t)s * 2 * Lu;
+        const int nfuse = ((a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC) && (MODE & MODE_RANSAC))
+                              ? min(nchunks, a.corg_cap) : 0;
+        auto lmk_fn = [&](int j, double &px, double &py) {
+            px = lm[2 * j];
+            py = lm[2 * j + 1];
+            if (j < nfuse) {
+                const double2 q = corg[j];
+                if (q.x == q.x) { px = q.x; py = q.y; }
+            }
+        };
+        UkfLds us;
+        us.carve((double *)(smem + a.off_ukf), Lu);
+        ukf_step(x, Pm, u[0], u[1], B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, us, lane);
+        if (lane == 0) {
+            for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = x[i];
+            for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
+        }
+    }
+}
+
+// A1: polar -> Cartesian (functions.py:59-60)
+__global__ __launch_bounds__(256) void polar_kernel(const double *__restrict__ th, const double *__restrict__ d,
+                                                    double2 *__restrict__ xy, int64_t n) {
+    const double A = LS_PI / 180.0;
+    const double H = LS_PI / 2.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double ang = -th[i] * A + H;
+        const double di = d[i];
+        xy[i] = make_double2(di * cos(ang), di * sin(ang));
+    }
+}
+
+// ------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------
+constexpr int LSLAM_EV_RING = 64;
+
+struct lslam_ctx {
+    int device;
+    hipStream_t stream;
+    bool timing;
+    // per kernel id: a ring of (start, stop) event pairs harvested lazily, so
+    // timing never blocks the host between back-to-back launches
+    hipEvent_t ev0[LSLAM_K_COUNT][LSLAM_EV_RING], ev1[LSLAM_K_COUNT][LSLAM_EV_RING];
+    int head[LSLAM_K_COUNT], npend[LSLAM_K_COUNT];
+    double total_ms[LSLAM_K_COUNT];
+    int64_t launches[LSLAM_K_COUNT];
+};
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const char *msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess) {                                                       \
+            g_err = std::string(#expr) + ": " + hipGetErrorString(_e);                \
+            return LSLAM_ERR_HIP;                                                     \
+        }                                                                             \
+    } while (0)
+
+extern "C" {
+
+const char *lslam_version(void) { return "lidarslam-mi355x 0.1.0 (abi 1, gfx950)"; }
+
+const char *lslam_status_string(int st) {
+    switch (st) {
+        case LSLAM_OK: return "ok";
+        case LSLAM_ERR_ARG: return "invalid argument";
+        case LSLAM_ERR_HIP: return "HIP runtime error";
+        case LSLAM_ERR_NOMEM: return "out of memory";
+        case LSLAM_ERR_CAPACITY: return "capacity exceeded";
+        case LSLAM_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+const char *lslam_last_error(void) { return g_err.c_str(); }
+
+int lslam_device_count(int *n) {
+    if (!n) return LSLAM_ERR_ARG;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *n = c;
+    return LSLAM_OK;
+}
+
+int lslam_ctx_create(int device, lslam_ctx **out) {
+    if (!out) return LSLAM_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return set_err(LSLAM_ERR_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    lslam_ctx *c = new (std::nothrow) lslam_ctx();
+    if (!c) return LSLAM_ERR_NOMEM;
+    c->device = device;
+    c->timing = false;
+    for (int k = 0; k < LSLAM_K_COUNT; k++) {
+        c->total_ms[k] = 0;
+        c->launches[k] = 0;
+        c->head[k] = 0;
+        c->npend[k] = 0;
+        for (int r = 0; r < LSLAM_EV_RING; r++) c->ev0[k][r] = c->ev1[k][r] = nullptr;
+    }
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return set_err(LSLAM_ERR_HIP, hipGetErrorString(e));
+    }
+    for (int k = 0; k < LSLAM_K_COUNT; k++)
+        for (int r = 0; r < LSLAM_EV_RING; r++) {
+            HIPCHK(hipEventCreate(&c->ev0[k][r]));
+            HIPCHK(hipEventCreate(&c->ev1[k][r]));
+        }
+    *out = c;
+    return LSLAM_OK;
+}
+
+int lslam_ctx_destroy(lslam_ctx *c) {
+    if (!c) return LSLAM_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (int k = 0; k < LSLAM_K_COUNT; k++)
+        for (int r = 0; r < LSLAM_EV_RING; r++) {
+            if (c->ev0[k][r]) (void)hipEventDestroy(c->ev0[k][r]);
+            if (c->ev1[k][r]) (void)hipEventDestroy(c->ev1[k][r]);
+        }
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return LSLAM_OK;
+}
+
+int lslam_sync(lslam_ctx *c) {
+    if (!c) return LSLAM_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return LSLAM_OK;
+}
+
+int lslam_malloc(lslam_ctx *c, size_t bytes, void **p) {
+    if (!c || !p) return LSLAM_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory");
+    HIPCHK(e);
+    return LSLAM_OK;
+}
+
+int lslam_free(lslam_ctx *c, void *p) {
+    if (!c) return LSLAM_ERR_ARG;
+    if (!p) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipFree(p));
+    return LSLAM_OK;
+}
+
+int lslam_host_alloc(size_t bytes, void **p) {
+    if (!p) return LSLAM_ERR_ARG;
+    HIPCHK(hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault));
+    return LSLAM_OK;
+}
+
+int lslam_host_free(void *p) {
+    if (p) HIPCHK(hipHostFree(p));
+    return LSLAM_OK;
+}
+
+int lslam_h2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
+    if (!n) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+    return LSLAM_OK;
+}
+
+int lslam_d2h(lslam_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
+    if (!n) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+    return LSLAM_OK;
+}
+
+int lslam_memset(lslam_ctx *c, void *dst, int v, size_t n) {
+    if (!c || (!dst && n)) return LSLAM_ERR_ARG;
+    if (!n) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(dst, v, n, c->stream));
+    return LSLAM_OK;
+}
+
+// fold the oldest `keep_free` pending event pairs (all of them if < 0) into the totals
+static int harvest(lslam_ctx *c, int k, int upto_free = -1) {
+    while (c->npend[k] > 0 && (upto_free < 0 || LSLAM_EV_RING - c->npend[k] < upto_free)) {
+        const int r = (c->head[k] - c->npend[k] + LSLAM_EV_RING) % LSLAM_EV_RING;
+        HIPCHK(hipEventSynchronize(c->ev1[k][r]));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev0[k][r], c->ev1[k][r]));
+        c->total_ms[k] += ms;
+        c->launches[k] += 1;
+        c->npend[k] -= 1;
+    }
+    return LSLAM_OK;
+}
+
+static int timer_begin(lslam_ctx *c, int k) {
+    if (!c->timing) return LSLAM_OK;
+    int st = harvest(c, k, 1);
+    if (st) return st;
+    HIPCHK(hipEventRecord(c->ev0[k][c->head[k]], c->stream));
+    return LSLAM_OK;
+}
+
+static int timer_end(lslam_ctx *c, int k) {
+    if (!c->timing) return LSLAM_OK;
+    HIPCHK(hipEventRecord(c->ev1[k][c->head[k]], c->stream));
+    c->head[k] = (c->head[k] + 1) % LSLAM_EV_RING;
+    c->npend[k] += 1;
+    return LSLAM_OK;
+}
+
+int lslam_set_timing(lslam_ctx *c, int en) {
+    if (!c) return LSLAM_ERR_ARG;
+    c->timing = en != 0;
+    return LSLAM_OK;
+}
+
+int lslam_timing(lslam_ctx *c, int k, double *ms, int64_t *n) {
+    if (!c || k < 0 || k >= LSLAM_K_COUNT) return LSLAM_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    int st = harvest(c, k);
+    if (st) return st;
+    if (ms) *ms = c->total_ms[k];
+    if (n) *n = c->launches[k];
+    return LSLAM_OK;
+}
+
+int lslam_timing_reset(lslam_ctx *c) {
+    if (!c) return LSLAM_ERR_ARG;
+    for (int k = 0; k < LSLAM_K_COUNT; k++) {
+        int st = harvest(c, k);
+        if (st) return st;
+        c->total_ms[k] = 0;
+        c->launches[k] = 0;
+    }
+    return LSLAM_OK;
+}
+
+int lslam_ransac_params_default(lslam_ransac_params *p) {
+    if (!p) return LSLAM_ERR_ARG;
+    memset(p, 0, sizeof(*p));
+    p->residual_threshold = 20.0;  // ransac_functions.py:9
+    p->max_trials = 100;           // :10
+    p->min_samples = 2;            // :11
+    p->hyp_source = LSLAM_HYP_MT19937;
+    p->life = 40;                  // landmarking.py:3
+    p->tol_a = 0.1;                // :4
+    p->tol_b = 10.0;               // :5
+    p->tol_dist = 100.0;           // :6
+    p->philox_seed = 0x5eed5eedull;
+    return LSLAM_OK;
+}
+
+int lslam_ukf_params_default(lslam_ukf_params *p, int32_t L) {
+    if (!p || L < 0) return LSLAM_ERR_ARG;
+    memset(p, 0, sizeof(*p));
+    p->n_landmarks = L;
+    p->flags = LSLAM_UKF_PREDICT | LSLAM_UKF_UPDATE;
+    p->dt = 0.005;          // systemClass.py:10
+    p->wheel_radius = 50;   // UKFMethods.py:6
+    p->wheel_base = 200;    // UKFMethods.py:7
+    p->alpha = 1e-4;        // systemClass.py:20
+    p->beta = 2.0;
+    p->kappa = 0.0;
+    for (int i = 0; i < 9; i++) p->Q[i] = (i % 4 == 0) ? 0.001 : 0.0;  // systemClass.py:29
+    return LSLAM_OK;
+}
+
+double lslam_inlier_cutoff(double thr) {
+    if (isnan(thr)) return NAN;
+    if (!(thr > 0)) return 0.0;
+    if (isinf(thr)) return INFINITY;
+    double e = thr * thr;
+    while (e > 0 && sqrt(e) >= thr) e = nextafter(e, 0.0);
+    while (sqrt(e) < thr) e = nextafter(e, INFINITY);
+    return e;
+}
+
+int lslam_ukf_weights(const lslam_ukf_params *p, double *Wm, double *Wc, double *lpn) {
+    if (!p || !Wm || !Wc) return LSLAM_ERR_ARG;
+    // filterpy MerweScaledSigmaPoints._compute_weights, n = 3
+    const double n = 3.0;
+    const double lambda_ = p->alpha * p->alpha * (n + p->kappa) - n;
+    const double c = .5 / (n + lambda_);
+    for (int i = 0; i < 7; i++) Wm[i] = Wc[i] = c;
+    Wc[0] = lambda_ / (n + lambda_) + (1 - p->alpha * p->alpha + p->beta);
+    Wm[0] = lambda_ / (n + lambda_);
+    if (lpn) *lpn = lambda_ + n;
+    return LSLAM_OK;
+}
+
+int lslam_mt_seed_state(uint32_t seed, uint32_t *st) {
+    if (!st) return LSLAM_ERR_ARG;
+    for (int i = 0; i < 624; i++) {
+        st[i] = seed;
+        seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(i + 1);
+    }
+    st[624] = 624;
+    return LSLAM_OK;
+}
+
+}  // extern "C"
+
+// ---- launch plumbing ----
+static inline int align16(int x) { return (x + 15) & ~15; }
+
+static int validate_batch(const lslam_scan_batch *b, bool need_points) {
+    if (!b) return set_err(LSLAM_ERR_ARG, "batch is NULL");
+    if (b->n_scans < 0 || b->n_chunks < 0 || b->n_points < 0) return set_err(LSLAM_ERR_ARG, "negative sizes");
+    if (b->n_scans == 0) return LSLAM_OK;
+    if (!b->scan_chunk_off || !b->chunk_pt_off) return set_err(LSLAM_ERR_ARG, "missing CSR offsets");
+    if (need_points && !b->xy && b->n_points > 0) return set_err(LSLAM_ERR_ARG, "missing xy");
+    if (b->max_chunk_points < 0 || b->max_scan_chunks < 0) return set_err(LSLAM_ERR_ARG, "bad maxima");
+    return LSLAM_OK;
+}
+
+static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_params *p, const lslam_ukf_params *u,
+                      int mode, int &lds) {
+    memset(&k, 0, sizeof(k));
+    k.b = *b;
+    if (p) {
+        if (p->min_samples != 2) return set_err(LSLAM_ERR_UNSUPPORTED, "only min_samples == 2 (ransac_functions.py:11)");
+        if (p->residual_threshold < 0) return set_err(LSLAM_ERR_ARG, "`residual_threshold` must be greater than zero");
+        if (p->max_trials < 0) return set_err(LSLAM_ERR_ARG, "`max_trials` must be greater than zero");
+        if (p->hyp_source < 0 || p->hyp_source > 2) return set_err(LSLAM_ERR_ARG, "bad hyp_source");
+        if (p->hyp_source == LSLAM_HYP_EXPLICIT && !b->hyp) return set_err(LSLAM_ERR_ARG, "explicit hyp without hyp");
+        k.thr = p->residual_threshold;
+        k.ecut = lslam_inlier_cutoff(p->residual_threshold);
+        k.tol_a = p->tol_a;
+        k.tol_b = p->tol_b;
+        k.tol_dist = p->tol_dist;
+        k.philox_seed = p->philox_seed;
+        k.T = p->max_trials;
+        k.hyp_source = p->hyp_source;
+        k.life = p->life;
+    }
+    if ((mode & MODE_ASSOC) && b->landmarks && !b->lmk_count) return set_err(LSLAM_ERR_ARG, "landmarks without lmk_count");
+    const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
+    const int T = k.T;
+    int off = 0;
+    k.off_pts = off; off += align16(16 * N);
+    k.off_key = off; off += align16(4 * 624);
+    uint32_t ring = 64;
+    while (ring < (uint32_t)(N + 64)) ring <<= 1;
+    k.ring_mask = ring - 1;
+    // phase-exclusive scratch shares one region: the J ring (draw generation),
+    // then the tie sums (selection), then the inlier list (mask + refit)
+    const int uni_bytes = max(max(2 * (int)ring, 8 * (T > 0 ? T : 1)), 4 * N);
+    k.off_ring = off;
+    k.off_tsum = off;
+    k.off_inl = off;
+    off += align16(uni_bytes);
+    k.off_draws = off; off += align16(8 * (T + 1));
+    k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
+    k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
+    k.off_mask = off; off += align16(N);
+    k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
+    k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+    k.hist_cap = b->max_scan_chunks > 0 ? b->max_scan_chunks : 1;
+    k.off_hist = off; off += align16(4 * k.hist_cap);
+    k.corg_cap = k.hist_cap;
+    k.off_corg = off; off += align16(16 * k.corg_cap);
+    k.lmk_cap = (mode & MODE_ASSOC) ? b->lmk_capacity : 0;
+    if ((mode & MODE_ASSOC) && k.lmk_cap <= 0) return set_err(LSLAM_ERR_ARG, "lmk_capacity must be > 0");
+    k.off_lmk = off; off += align16((int)sizeof(lslam_landmark) * (k.lmk_cap > 0 ? k.lmk_cap : 1));
+    k.off_vis = off; off += align16(8 * ((k.lmk_cap + 63) / 64 + 1));
+    k.pts_cap = N;
+    if (u) {
+        if (u->n_landmarks <= 0) return set_err(LSLAM_ERR_ARG, "n_landmarks must be > 0");
+        if (!b->ukf_x || !b->ukf_P || !b->ukf_u || !b->ukf_z || !b->ukf_lmk || !b->ukf_R_diag)
+            return set_err(LSLAM_ERR_ARG, "UKF buffers missing");
+        double lpn = 0;
+        lslam_ukf_weights(u, k.ukf.Wm, k.ukf.Wc, &lpn);
+        for (int i = 0; i < 7; i++)
+            if (k.ukf.Wc[i] == 0.0) return set_err(LSLAM_ERR_UNSUPPORTED, "zero covariance weight");
+        k.ukf.cfac = lpn;
+        k.ukf.dt = u->dt;
+        k.ukf.wr = u->wheel_radius;
+        k.ukf.wb = u->wheel_base;
+        for (int i = 0; i < 9; i++) k.ukf.Q[i] = u->Q[i];
+        k.ukf.L = u->n_landmarks;
+        k.ukf.flags = u->flags;
+        k.off_ukf = off;
+        off += align16(8 * UkfLds::doubles(u->n_landmarks));
+    }
+    lds = off;
+    if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk/trial/landmark sizes exceed the 160 KiB LDS");
+    return LSLAM_OK;
+}
+
+template <int MODE>
+static hipError_t launch_mode(const KArgs &k, int lds, hipStream_t st) {
+    const dim3 grid((unsigned)k.b.n_scans), block(64);
+    switch (k.hyp_source) {
+        case LSLAM_HYP_PHILOX:
+            hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_PHILOX, MODE>), grid, block, lds, st, k);
+            break;
+        case LSLAM_HYP_EXPLICIT:
+            hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, block, lds, st, k);
+            break;
+        default:
+            hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE>), grid, block, lds, st, k);
+            break;
+    }
+    return hipGetLastError();
+}
+
+template <int MODE>
+static int run_scan_kernel(lslam_ctx *c, const KArgs &k, int lds, int timer) {
+    HIPCHK(hipSetDevice(c->device));
+    if (k.b.n_scans == 0) return LSLAM_OK;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const int mx = 160 * 1024;
+        (void)hipFuncSetAttribute((const void *)scan_kernel<0, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipFuncSetAttribute((const void *)scan_kernel<1, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipFuncSetAttribute((const void *)scan_kernel<2, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    });
+    int st = timer_begin(c, timer);
+    if (st) return st;
+    HIPCHK(launch_mode<MODE>(k, lds, c->stream));
+    st = timer_end(c, timer);
+    if (st) return st;
+    return LSLAM_OK;
+}
+
+extern "C" {
+
+int lslam_polar_to_xy(lslam_ctx *c, const double *th, const double *d, double *xy, int64_t n) {
+    if (!c || n < 0 || (n > 0 && (!th || !d || !xy))) return LSLAM_ERR_ARG;
+    if (n == 0) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    int st = timer_begin(c, LSLAM_K_POLAR);
+    if (st) return st;
+    hipLaunchKernelGGL(polar_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, th, d, (double2 *)xy, n);
+    HIPCHK(hipGetLastError());
+    st = timer_end(c, LSLAM_K_POLAR);
+    if (st) return st;
+    return LSLAM_OK;
+}
+
+int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trials) {
+    if (!c) return LSLAM_ERR_ARG;
+    int st = validate_batch(b, false);
+    if (st) return st;
+    if (!b->draws_out) return set_err(LSLAM_ERR_ARG, "draws_out required");
+    lslam_ransac_params p;
+    lslam_ransac_params_default(&p);
+    p.max_trials = max_trials;
+    KArgs k;
+    int lds = 0;
+    st = build_args(k, b, &p, nullptr, MODE_HYP_ONLY, lds);
+    if (st) return st;
+    return run_scan_kernel<MODE_HYP_ONLY>(c, k, lds, LSLAM_K_HYP);
+}
+
+int lslam_ransac(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p) {
+    if (!c || !p) return LSLAM_ERR_ARG;
+    int st = validate_batch(b, true);
+    if (st) return st;
+    KArgs k;
+    int lds = 0;
+    st = build_args(k, b, p, nullptr, MODE_RANSAC, lds);
+    if (st) return st;
+    return run_scan_kernel<MODE_RANSAC>(c, k, lds, LSLAM_K_PIPELINE);
+}
+
+int lslam_landmarks(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p) {
+    if (!c || !p) return LSLAM_ERR_ARG;
+    int st = validate_batch(b, true);
+    if (st) return st;
+    if (!b->models || !b->landmarks || !b->inlier_mask) return set_err(LSLAM_ERR_ARG, "models/landmarks/mask required");
+    KArgs k;
+    int lds = 0;
+    st = build_args(k, b, p, nullptr, MODE_ASSOC, lds);
+    if (st) return st;
+    return run_scan_kernel<MODE_ASSOC>(c, k, lds, LSLAM_K_LANDMARK);
+}
+
+int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u) {
+    if (!c || !u || !b) return LSLAM_ERR_ARG;
+    if (b->n_scans < 0) return LSLAM_ERR_ARG;
+    lslam_scan_batch bb = *b;
+    // UKF-only: no chunks are touched; give the kernel an empty CSR if absent
+    KArgs k;
+    int lds = 0;
+    if (!bb.scan_chunk_off) return set_err(LSLAM_ERR_ARG, "scan_chunk_off required (may describe 0 chunks)");
+    int st = build_args(k, &bb, nullptr, u, MODE_UKF, lds);
+    if (st) return st;
+    return run_scan_kernel<MODE_UKF>(c, k, lds, LSLAM_K_UKF);
+}
+
+int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p,
+                        const lslam_ukf_params *u) {
+    if (!c || !p) return LSLAM_ERR_ARG;
+    int st = validate_batch(b, true);
+    if (st) return st;
+    KArgs k;
+    int lds = 0;
+    const bool assoc = b->landmarks != nullptr;
+    const int mode = MODE_RANSAC | (assoc ? MODE_ASSOC : 0) | (u ? MODE_UKF : 0);
+    st = build_args(k, b, p, u, mode, lds);
+    if (st) return st;
+    switch (mode) {
+        case MODE_RANSAC | MODE_ASSOC | MODE_UKF:
+            return run_scan_kernel<MODE_RANSAC | MODE_ASSOC | MODE_UKF>(c, k, lds, LSLAM_K_PIPELINE);
+        case MODE_RANSAC | MODE_UKF: return run_scan_kernel<MODE_RANSAC | MODE_UKF>(c, k, lds, LSLAM_K_PIPELINE);
+        case MODE_RANSAC | MODE_ASSOC: return run_scan_kernel<MODE_RANSAC | MODE_ASSOC>(c, k, lds, LSLAM_K_PIPELINE);
+        default: return run_scan_kernel<MODE_RANSAC>(c, k, lds, LSLAM_K_PIPELINE);
+    }
+}
+
+}  // extern "C"

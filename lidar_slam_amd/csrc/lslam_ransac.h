@@ -1,0 +1,138 @@
+// lslam_ransac.h — one RANSAC call per chunk on one wave.
+//
+// Arithmetic is the reference's, op for op (compile with -ffp-contract=off):
+//   LineModelND.estimate on 2 points   fit.py:84-91
+//     o = (p0 + p1) / 2 ; d = (p1 - o) - (p0 - o) ; n = sqrt(fma(dy,dy, dx*dx))
+//     u = d / n  (n != 0), else u = d
+//   LineModelND.residuals               fit.py:19-21,129-132
+//     t = fma(ex,ux, ey*uy)  [OpenBLAS dgemv_t rounding]
+//     r^2 = (ex - t*ux)^2 + (ey - t*uy)^2   [einsum, no FMA]
+//   inlier <=> sqrt(r^2) < thr  <=>  r^2 < ecut   (ecut = lslam_inlier_cutoff(thr))
+//   tie-break sum = numpy pairwise_sum of RN(sqrt(r^2))^2 over all N points
+//   selection fit.py:850-869, stop_residuals_sum=0 stop, final refit fit.py:871-875
+// Layout: the chunk's points are staged in LDS as double2; pass 1 puts one
+// hypothesis per lane and streams the points as LDS broadcasts (no bank
+// conflicts, points stay uniform, every lane runs the same FP64 chain).
+#pragma once
+#include "lslam_wave.h"
+
+namespace lslam {
+
+struct Model {
+    double ox, oy, ux, uy;
+};
+
+__device__ __forceinline__ Model model2(double2 p0, double2 p1) {
+    Model m;
+    m.ox = (p0.x + p1.x) / 2.0;
+    m.oy = (p0.y + p1.y) / 2.0;
+    const double d0x = p0.x - m.ox, d0y = p0.y - m.oy;
+    const double d1x = p1.x - m.ox, d1y = p1.y - m.oy;
+    double dx = d1x - d0x, dy = d1y - d0y;
+    const double nrm = cr_sqrt(__builtin_fma(dy, dy, dx * dx));
+    if (nrm != 0.0) {
+        dx = dx / nrm;
+        dy = dy / nrm;
+    }
+    m.ux = dx;
+    m.uy = dy;
+    return m;
+}
+
+__device__ __forceinline__ double resid2(double2 p, const Model &m) {
+    const double ex = p.x - m.ox, ey = p.y - m.oy;
+    const double t = __builtin_fma(ex, m.ux, ey * m.uy);
+    const double rx = ex - t * m.ux, ry = ey - t * m.uy;
+    return rx * rx + ry * ry;
+}
+
+__device__ __forceinline__ double r2sq(double2 p, const Model &m) {
+    const double r = cr_sqrt(resid2(p, m));
+    return r * r;
+}
+
+// numpy pairwise_sum leaf (n <= 128) of r^2 over P[start .. start+n)
+__device__ __forceinline__ double pw_leaf(const double2 *P, int start, int n, const Model &m) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; i++) res += r2sq(P[start + i], m);
+        return res;
+    }
+    double r0 = r2sq(P[start + 0], m), r1 = r2sq(P[start + 1], m), r2 = r2sq(P[start + 2], m),
+           r3 = r2sq(P[start + 3], m), r4 = r2sq(P[start + 4], m), r5 = r2sq(P[start + 5], m),
+           r6 = r2sq(P[start + 6], m), r7 = r2sq(P[start + 7], m);
+    int i = 8;
+    const int lim = n - (n % 8);
+    for (; i < lim; i += 8) {
+        r0 += r2sq(P[start + i + 0], m);
+        r1 += r2sq(P[start + i + 1], m);
+        r2 += r2sq(P[start + i + 2], m);
+        r3 += r2sq(P[start + i + 3], m);
+        r4 += r2sq(P[start + i + 4], m);
+        r5 += r2sq(P[start + i + 5], m);
+        r6 += r2sq(P[start + i + 6], m);
+        r7 += r2sq(P[start + i + 7], m);
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) res += r2sq(P[start + i], m);
+    return res;
+}
+
+// numpy pairwise_sum for any n: the recursion (n2 = n/2 - (n/2)%8) is walked
+// iteratively; the node stack is wave-uniform (same n for every lane) and the
+// per-lane partial sums live in an LDS stack vstack[depth*64 + lane];
+// nstack (LDS, 3*24 ints) holds the uniform node stack (all lanes write the
+// same values).  Depth <= 24 covers any n < 2^30.
+__device__ __forceinline__ double pw_sum(const double2 *P, int n, const Model &m, double *vstack,
+                                         int *nstack, int lane) {
+    if (n <= 128) return pw_leaf(P, 0, n, m);
+    // explicit DFS: node = (start, len, state); state 0 = descend left, 1 = descend right, 2 = combine
+    int *st_start = nstack, *st_len = nstack + 24, *st_state = nstack + 48;
+    int sp = 0;
+    st_start[0] = 0; st_len[0] = n; st_state[0] = 0;
+    int vsp = 0;
+    while (sp >= 0) {
+        const int s0 = st_start[sp], ln = st_len[sp];
+        if (ln <= 128) {
+            vstack[vsp * 64 + lane] = pw_leaf(P, s0, ln, m);
+            vsp++;
+            sp--;
+            continue;
+        }
+        int n2 = ln / 2;
+        n2 -= n2 % 8;
+        if (st_state[sp] == 0) {
+            st_state[sp] = 1;
+            sp++;
+            st_start[sp] = s0; st_len[sp] = n2; st_state[sp] = 0;
+        } else if (st_state[sp] == 1) {
+            st_state[sp] = 2;
+            sp++;
+            st_start[sp] = s0 + n2; st_len[sp] = ln - n2; st_state[sp] = 0;
+        } else {
+            const double right = vstack[(vsp - 1) * 64 + lane];
+            const double left = vstack[(vsp - 2) * 64 + lane];
+            vsp -= 2;
+            vstack[vsp * 64 + lane] = left + right;
+            vsp++;
+            sp--;
+        }
+    }
+    return vstack[lane];
+}
+
+// closed-form principal direction of the centred inliers (replaces dgesdd's
+// v[0], fit.py:94); identical formula in oracle/ransac_oracle.c
+__device__ __forceinline__ void tls_direction(double sxx, double sxy, double syy, double &ux, double &uy) {
+    const double h = (sxx - syy) * 0.5;
+    const double r = cr_sqrt(h * h + sxy * sxy);
+    double vx, vy;
+    if (sxx >= syy) { vx = h + r; vy = sxy; }
+    else { vx = sxy; vy = r - h; }
+    const double nv = cr_sqrt(vx * vx + vy * vy);
+    if (!(nv > 0.0)) { ux = 1.0; uy = 0.0; return; }
+    ux = vx / nv;
+    uy = vy / nv;
+}
+
+}  // namespace lslam

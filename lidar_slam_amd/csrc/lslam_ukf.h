@@ -1,0 +1,317 @@
+// lslam_ukf.h — one UKF predict/update per scan on one wave.
+//
+// Semantics: the INTENT of UKFMethods.py:10-71 + systemClass.py:7-29 (both files
+// fail to parse in the reference) run through filterpy 1.4.5's
+// UnscentedKalmanFilter (absent from the container; restated).  PARITY
+// UNPINNED — checked against the NumPy restatement in oracle/ukf.py.
+//
+//   sigma points  MerweScaled: U = chol_upper((lambda+n) P); s0 = x,
+//                 s_{1+k} = x + U[k], s_{4+k} = x - U[k]
+//   fx            x + dt * B(theta) u,  B = [[R/2 c, R/2 c],[R/2 s, R/2 s],[-R/L, R/L]]
+//   hx            per landmark j: [sqrt(dx^2+dy^2), wrap(atan2(dy,dx) - theta)]
+//   means         linear weighted sums; angles by atan2(sum W sin, sum W cos)
+//   residuals     differences with angle components wrapped to (-pi, pi]
+//   predict       x, P = UT(fx(sigmas)) + Q; sigmas_f re-drawn from (x, P)
+//   update        S = sum Wc rz rz^T + R, Pxz = sum Wc rx rz^T, K = Pxz S^-1,
+//                 x += K y, P -= K S K^T
+// The update is evaluated in its exact rank-7 (Woodbury) form, so no 2L x 2L
+// matrix is ever formed (L = 200 -> dim_z = 400 stays a 7x7 solve):
+//   with Y = [rz_k] (7 x m), Dx = [rx_k] (7 x 3), W = diag(Wc), G = Y R^-1 Y^T,
+//   M = W^-1 + G:   K y = Dx^T M^-1 (Y R^-1 y),   K S K^T = Dx^T (W - M^-1) Dx.
+// Work split: lane k < 7 owns sigma point k (fx), lanes own landmarks for hx,
+// lanes own G entries for the 7x7 products, lanes own matrix entries in the
+// Gauss-Jordan solve; small uniform values are exchanged through LDS.
+#pragma once
+#include "lslam_wave.h"
+
+namespace lslam {
+
+constexpr double LS_PI = 3.141592653589793;
+constexpr double LS_TWO_PI = 6.283185307179586;
+
+// UKFMethods.py:10-14 normalize_angle: Python float % (floor-mod), then -2pi above pi
+__device__ __forceinline__ double wrap_angle(double a) {
+    double m = fmod(a, LS_TWO_PI);
+    if (m != 0.0) {
+        if (m < 0.0) m += LS_TWO_PI;
+    } else {
+        m = 0.0;
+    }
+    if (m > LS_PI) m -= LS_TWO_PI;
+    return m;
+}
+
+struct UkfConst {
+    double Wm[7], Wc[7];
+    double cfac;  // lambda + n
+    double dt, wr, wb;
+    double Q[9];
+    int L;
+    int flags;
+};
+
+// LDS scratch layout for one wave's UKF step (doubles)
+struct UkfLds {
+    double *sig;   // [7][3]
+    double *Dx;    // [7][3]
+    double *aug;   // [7][14]  [M | I] -> [I | M^-1]
+    double *G;     // [28]
+    double *bv;    // [7]
+    double *xv;    // [16] x(3) P(9) misc
+    double *Y;     // [7][2L] measurement residuals rz_k
+    double *yr;    // [2L] innovation residual_h(z, zp)
+    static __host__ __device__ int doubles(int L) { return 21 + 21 + 98 + 28 + 7 + 16 + 7 * 2 * L + 2 * L; }
+    __device__ void carve(double *base, int L) {
+        sig = base; Dx = sig + 21; aug = Dx + 21; G = aug + 98; bv = G + 28; xv = bv + 7; Y = xv + 16;
+        yr = Y + 7 * 2 * L;
+    }
+};
+
+// LAPACK dpotrf('U') on a 3x3 SPD matrix (recursive dpotrf2 order)
+__device__ __forceinline__ void chol3_upper(const double A[9], double U[9]) {
+    U[0] = cr_sqrt(A[0]);
+    U[1] = A[1] / U[0];
+    U[2] = A[2] / U[0];
+    U[3] = 0.0;
+    U[4] = cr_sqrt(A[4] - U[1] * U[1]);
+    U[5] = (A[5] - U[1] * U[2]) / U[4];
+    U[6] = 0.0;
+    U[7] = 0.0;
+    U[8] = cr_sqrt((A[8] - U[2] * U[2]) - U[5] * U[5]);
+}
+
+// sigma point k of MerweScaledSigmaPoints.sigma_points(x, P)
+__device__ __forceinline__ void sigma_point(int k, const double x[3], const double U[9], double o[3]) {
+    for (int j = 0; j < 3; j++) {
+        if (k == 0) o[j] = x[j];
+        else if (k <= 3) o[j] = x[j] - (-U[3 * (k - 1) + j]);
+        else o[j] = x[j] - U[3 * (k - 4) + j];
+    }
+}
+
+// UKFMethods.py:17-24 transition_function (intended form)
+__device__ __forceinline__ void fx(const double s[3], double dt, double u0, double u1, double wr, double wb,
+                                   double o[3]) {
+    const double c = (wr / 2.0) * cos(s[2]);
+    const double sn = (wr / 2.0) * sin(s[2]);
+    const double k0 = (-1.0 * wr) / wb, k1 = (1.0 * wr) / wb;
+    const double b0 = c * u0 + c * u1;
+    const double b1 = sn * u0 + sn * u1;
+    const double b2 = k0 * u0 + k1 * u1;
+    o[0] = s[0] + dt * b0;
+    o[1] = s[1] + dt * b1;
+    o[2] = s[2] + dt * b2;
+}
+
+// One UKF step for one scan; x[3], P[9] in/out (uniform).  Returns false if a
+// factorisation failed (non-SPD P or singular M).
+template <typename LmkFn>
+__device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const double *z, const double *Rd,
+                         LmkFn lmk, const UkfConst &C, UkfLds &S, int lane) {
+    bool ok = true;
+    double U[9];
+    if (C.flags & 1) {  // ---- predict (filterpy UKF.predict)
+        {
+            double A[9];
+            for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
+            chol3_upper(A, U);
+        }
+        if (lane < 7) {
+            double sg[3], o[3];
+            sigma_point(lane, x, U, sg);
+            fx(sg, C.dt, u0, u1, C.wr, C.wb, o);
+            S.sig[3 * lane] = o[0];
+            S.sig[3 * lane + 1] = o[1];
+            S.sig[3 * lane + 2] = o[2];
+        }
+        __syncthreads();
+        // UKFMethods.py:37-45 state_mean (intended form)
+        double s0 = 0.0, s1 = 0.0, ss = 0.0, sc = 0.0;
+        for (int k = 0; k < 7; k++) {
+            const double a0 = S.sig[3 * k], a1 = S.sig[3 * k + 1], a2 = S.sig[3 * k + 2];
+            s0 += a0 * C.Wm[k];
+            s1 += a1 * C.Wm[k];
+            ss += sin(a2) * C.Wm[k];
+            sc += cos(a2) * C.Wm[k];
+        }
+        const double xm0 = s0, xm1 = s1, xm2 = atan2(ss, sc);
+        // unscented_transform with residual_x (loop form) + Q
+        double Pn[9];
+        for (int i = 0; i < 9; i++) Pn[i] = 0.0;
+        for (int k = 0; k < 7; k++) {
+            const double y0 = S.sig[3 * k] - xm0, y1 = S.sig[3 * k + 1] - xm1;
+            const double y2 = wrap_angle(S.sig[3 * k + 2] - xm2);
+            const double y[3] = {y0, y1, y2};
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) Pn[3 * i + j] = Pn[3 * i + j] + C.Wc[k] * (y[i] * y[j]);
+        }
+        for (int i = 0; i < 9; i++) P[i] = Pn[i] + C.Q[i];
+        x[0] = xm0;
+        x[1] = xm1;
+        x[2] = xm2;
+        __syncthreads();
+    }
+    if (!(C.flags & 2)) return ok;
+    // ---- sigmas_f re-drawn from (x, P) (end of predict; also the update-only case)
+    {
+        double A[9];
+        for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
+        chol3_upper(A, U);
+        if (!(U[0] > 0.0) || !(U[4] > 0.0) || !(U[8] > 0.0)) ok = false;
+    }
+    if (lane < 7) {
+        double sg[3];
+        sigma_point(lane, x, U, sg);
+        S.sig[3 * lane] = sg[0];
+        S.sig[3 * lane + 1] = sg[1];
+        S.sig[3 * lane + 2] = sg[2];
+        S.Dx[3 * lane] = sg[0] - x[0];
+        S.Dx[3 * lane + 1] = sg[1] - x[1];
+        S.Dx[3 * lane + 2] = wrap_angle(sg[2] - x[2]);
+    }
+    __syncthreads();
+    // ---- hx over landmarks (lanes), z_mean, residuals -> Y, yr
+    const int m2 = 2 * C.L;
+    for (int j0 = 0; j0 < C.L; j0 += 64) {
+        const int j = j0 + lane;
+        if (j < C.L) {
+            double px, py;
+            lmk(j, px, py);
+            double d[7], ph[7];
+            for (int k = 0; k < 7; k++) {
+                const double dx = px - S.sig[3 * k], dy = py - S.sig[3 * k + 1];
+                d[k] = cr_sqrt(dx * dx + dy * dy);
+                ph[k] = wrap_angle(atan2(dy, dx) - S.sig[3 * k + 2]);
+            }
+            double dm = 0.0, ss = 0.0, sc = 0.0;
+            for (int k = 0; k < 7; k++) {
+                dm += d[k] * C.Wm[k];
+                ss += sin(ph[k]) * C.Wm[k];
+                sc += cos(ph[k]) * C.Wm[k];
+            }
+            const double pm = atan2(ss, sc);
+            for (int k = 0; k < 7; k++) {
+                S.Y[k * m2 + 2 * j] = d[k] - dm;
+                S.Y[k * m2 + 2 * j + 1] = wrap_angle(ph[k] - pm);
+            }
+            S.yr[2 * j] = z[2 * j] - dm;
+            S.yr[2 * j + 1] = wrap_angle(z[2 * j + 1] - pm);
+        }
+    }
+    __syncthreads();
+    // ---- G = Y R^-1 Y^T (28 upper entries, lanes 0..27), b = Y R^-1 y (lanes 28..34)
+    if (lane < 35) {
+        int k, l;
+        if (lane < 28) {
+            int e = lane;
+            k = 0;
+            while (e >= 7 - k) { e -= 7 - k; k++; }
+            l = k + e;
+        } else {
+            k = lane - 28;
+            l = -1;
+        }
+        double acc = 0.0;
+        const double *yk = S.Y + k * m2;
+        const double *yl = (l >= 0) ? S.Y + l * m2 : S.yr;
+        for (int m = 0; m < m2; m++) acc += (yk[m] / Rd[m]) * yl[m];
+        if (lane < 28) S.G[lane] = acc;
+        else S.bv[lane - 28] = acc;
+    }
+    __syncthreads();
+    // ---- M = W^-1 + G ; [M | I] in LDS
+    for (int e = lane; e < 98; e += 64) {
+        const int r = e / 14, cc = e % 14;
+        double v;
+        if (cc < 7) {
+            const int k = min(r, cc), l = max(r, cc);
+            const int idx = k * 7 - (k * (k - 1)) / 2 + (l - k);
+            v = S.G[idx];
+            if (r == cc) v += 1.0 / C.Wc[r];
+        } else {
+            v = (cc - 7 == r) ? 1.0 : 0.0;
+        }
+        S.aug[e] = v;
+    }
+    __syncthreads();
+    // ---- Gauss-Jordan with partial pivoting, lanes over entries
+    for (int c = 0; c < 7; c++) {
+        int piv = c;
+        double best = fabs(S.aug[c * 14 + c]);
+        for (int r = c + 1; r < 7; r++) {
+            const double v = fabs(S.aug[r * 14 + c]);
+            if (v > best) { best = v; piv = r; }
+        }
+        if (!(best > 0.0)) ok = false;
+        if (piv != c) {
+            double t0 = 0.0, t1 = 0.0;
+            if (lane < 14) { t0 = S.aug[c * 14 + lane]; t1 = S.aug[piv * 14 + lane]; }
+            __syncthreads();
+            if (lane < 14) { S.aug[c * 14 + lane] = t1; S.aug[piv * 14 + lane] = t0; }
+            __syncthreads();
+        }
+        const double dpiv = S.aug[c * 14 + c];
+        double rowc = 0.0;
+        if (lane < 14) rowc = S.aug[c * 14 + lane] / dpiv;
+        __syncthreads();
+        if (lane < 14) S.aug[c * 14 + lane] = rowc;
+        __syncthreads();
+        // eliminate column c from the other rows (lanes own entries e and e+64)
+        const int e0 = lane, e1 = lane + 64;
+        double v0, v1 = 0.0;
+        {
+            const int r = e0 / 14, cc = e0 % 14;
+            v0 = S.aug[e0];
+            if (r != c) {
+                const double f = S.aug[r * 14 + c];
+                if (f != 0.0) v0 = v0 - f * S.aug[c * 14 + cc];
+            }
+        }
+        if (e1 < 98) {
+            const int r = e1 / 14, cc = e1 % 14;
+            v1 = S.aug[e1];
+            if (r != c) {
+                const double f = S.aug[r * 14 + c];
+                if (f != 0.0) v1 = v1 - f * S.aug[c * 14 + cc];
+            }
+        }
+        __syncthreads();
+        S.aug[e0] = v0;
+        if (e1 < 98) S.aug[e1] = v1;
+        __syncthreads();
+    }
+    // Minv[k][l] = aug[k*14 + 7 + l]
+    // ---- x += Dx^T M^-1 b ;  P -= Dx^T (W - M^-1) Dx
+    double mb[7];
+    for (int k = 0; k < 7; k++) {
+        double s = 0.0;
+        for (int l = 0; l < 7; l++) s += S.aug[k * 14 + 7 + l] * S.bv[l];
+        mb[k] = s;
+    }
+    double dxn[3];
+    for (int i = 0; i < 3; i++) {
+        double s = 0.0;
+        for (int k = 0; k < 7; k++) s += S.Dx[3 * k + i] * mb[k];
+        dxn[i] = s;
+    }
+    double KSK[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0.0;
+            for (int k = 0; k < 7; k++) {
+                double t = 0.0;
+                for (int l = 0; l < 7; l++) {
+                    const double wml = ((k == l) ? C.Wc[k] : 0.0) - S.aug[k * 14 + 7 + l];
+                    t += wml * S.Dx[3 * l + j];
+                }
+                s += S.Dx[3 * k + i] * t;
+            }
+            KSK[3 * i + j] = s;
+        }
+    for (int i = 0; i < 3; i++) x[i] = x[i] + dxn[i];
+    for (int i = 0; i < 9; i++) P[i] = P[i] - KSK[i];
+    __syncthreads();
+    return ok;
+}
+
+}  // namespace lslam

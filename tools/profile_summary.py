@@ -1,0 +1,66 @@
+"""Summarise rocprofv3 outputs of tools/run_gpu.sh into profiles/.
+
+  python tools/profile_summary.py <tag>   (reads gpurun_out/, writes profiles/<tag>_*)
+
+Kernel time comes from --kernel-trace --stats; HBM traffic from separate
+--pmc FETCH_SIZE and --pmc WRITE_SIZE passes (MI355X_MICROARCH.md §HBM:
+FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes
+of a wide coalesced stream, so the read side is doubled).
+"""
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def counter(path, name, kernel_sub="scan_kernel"):
+    vals = [float(r["Counter_Value"]) for r in rows(path)
+            if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == name]
+    return vals
+
+
+def main(tag):
+    os.makedirs(PROF, exist_ok=True)
+    stats = rows(os.path.join(OUT, "prof_kt", "kt_kernel_stats.csv"))
+    bench = [json.loads(l) for l in open(os.path.join(OUT, "bench.json")) if l.startswith("{")][-1]
+    fetch = counter(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = counter(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
+    f_kib = sum(fetch) / len(fetch) if fetch else None
+    w_kib = sum(write) / len(write) if write else None
+    traffic = None
+    if f_kib is not None and w_kib is not None:
+        traffic = int(2 * f_kib * 1024 + w_kib * 1024)
+    lines = ["# rocprofv3 summary: %s" % tag, "",
+             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2`",
+             "(PMC: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes, --steps 3 --warmup 1)", "",
+             "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
+    for r in stats:
+        lines.append("| `%s` | %s | %.1f | %.1f | %.1f | %s |" % (
+            r["Name"], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3,
+            float(r["MaxNs"]) / 1e3, r["Percentage"]))
+    lines += ["", "PMC per scan_kernel launch: FETCH_SIZE %.1f KiB (x2 gfx950 correction), WRITE_SIZE %.1f KiB "
+              "-> traffic %s bytes/launch" % (f_kib or -1, w_kib or -1, traffic),
+              "", "bench.py line of the same build:", "", "```", json.dumps(bench), "```"]
+    open(os.path.join(PROF, "%s_rocprof.md" % tag), "w").write("\n".join(lines) + "\n")
+    for src in ("prof_kt/kt_kernel_stats.csv",):
+        data = open(os.path.join(OUT, src)).read()
+        open(os.path.join(PROF, "%s_%s" % (tag, os.path.basename(src))), "w").write(data)
+    t = {"tag": tag, "scans": bench["config"]["scans_per_gpu"], "hyp": bench["config"]["hyp"],
+         "fetch_kib": f_kib, "write_kib": w_kib, "bytes_per_launch": traffic,
+         "kernel_avg_us": [float(r["AverageNs"]) / 1e3 for r in stats if "scan_kernel" in r["Name"]]}
+    json.dump(t, open(os.path.join(PROF, "traffic_latest.json"), "w"), indent=1)
+    json.dump(bench, open(os.path.join(PROF, "%s_bench.json" % tag), "w"))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
