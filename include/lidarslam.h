@@ -56,7 +56,8 @@ enum {
     LSLAM_EARLY_STOP = 16,    /* stop_residuals_sum hit (sum of squared residuals == 0) */
     LSLAM_VERTICAL = 32,      /* final direction x == 0: a = +-inf/nan (ransac_functions.py:26) */
     LSLAM_NEW_LANDMARK = 64,  /* no landmark matched: the chunk's Landmark was appended */
-    LSLAM_MATCHED = 128       /* an existing landmark matched (its life reset to LIFE) */
+    LSLAM_MATCHED = 128,      /* an existing landmark matched (its life reset to LIFE) */
+    LSLAM_CAPACITY = 256      /* no match and the list was full: the new landmark was dropped */
 };
 
 /* ---- hypothesis sources ---- */
@@ -141,6 +142,10 @@ typedef struct lslam_scan_batch {
     const int32_t *id_base;         /* [n_scans] landmarkNumber of the first chunk (optional, 0) */
     lslam_landmark *landmarks;      /* [n_scans][lmk_capacity] in/out (optional) */
     int32_t *lmk_count;             /* [n_scans] in/out (required with landmarks) */
+    int32_t *lmk_walk;              /* [n_scans][lmk_capacity] out (optional): life of each entry of the
+                                       list as it was before the scan's LAST chunk, after that chunk's
+                                       association walk (0 = removed); lets a caller holding its own
+                                       list objects apply the walk (the drop-in shim) */
     /* outputs */
     uint8_t *inlier_mask;           /* [n_points] */
     lslam_chunk_model *models;      /* [n_chunks] */

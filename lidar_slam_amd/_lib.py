@@ -65,7 +65,7 @@ class ScanBatch(C.Structure):
                 ("max_chunk_points", C.c_int32), ("max_scan_chunks", C.c_int32), ("lmk_capacity", C.c_int32),
                 ("reserved", C.c_int32)] + \
                [(n, _VP) for n in ("xy", "scan_chunk_off", "chunk_pt_off", "seeds", "mt_state_in", "mt_state_out",
-                                   "hyp", "id_base", "landmarks", "lmk_count", "inlier_mask", "models", "y_proj",
+                                   "hyp", "id_base", "landmarks", "lmk_count", "lmk_walk", "inlier_mask", "models", "y_proj",
                                    "draws_out", "trial_cnt_out", "ukf_x", "ukf_P", "ukf_u", "ukf_z", "ukf_lmk",
                                    "ukf_R_diag")]
 

@@ -34,7 +34,6 @@ static_assert(sizeof(lslam_chunk_model) == 112, "chunk model ABI");
 static_assert(sizeof(lslam_landmark) == 56, "landmark ABI");
 
 enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8 };
-enum { LSLAM_CAPACITY_FLAG = 256 };
 
 // ------------------------------------------------------------------------
 // kernel arguments (passed by value)
@@ -254,7 +253,7 @@ __device__ __forceinline__ bool is_equal(const lslam_landmark &Lk, double a, dou
 // returns match index (pre-call) or -1; updates list + count; proj line out
 __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, int &L, double a, double b,
                          double px, double py, double ex, double ey, int id, double &pa, double &pb,
-                         bool &overflow, int lane) {
+                         bool &overflow, int32_t *walk_out, int lane) {
     const int nblk = (L + 63) >> 6;
     for (int i = lane; i < nblk; i += 64) vis[i] = 0ull;
     __syncthreads();
@@ -309,6 +308,7 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
                 keep = true;
             }
             if (j == match) e.life = ka.life;
+            if (walk_out) walk_out[j] = e.life;
         }
         const uint64_t km = ballot(keep);
         __syncthreads();
@@ -505,12 +505,13 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
                 double pa, pb;
                 bool overflow = false;
                 const int m = associate(a, lmk, vis, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
-                                        rec.landmark_id, pa, pb, overflow, lane);
+                                        rec.landmark_id, pa, pb, overflow,
+                                        B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr, lane);
                 rec.match_index = m;
                 rec.proj_a = pa;
                 rec.proj_b = pb;
                 rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
-                if (overflow) rec.flags |= LSLAM_CAPACITY_FLAG;
+                if (overflow) rec.flags |= LSLAM_CAPACITY;
             }
         }
         if (B.y_proj) {

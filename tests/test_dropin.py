@@ -1,0 +1,108 @@
+"""Drop-in surface tests.  CPU: the modules import and mirror the reference's
+names/constants; chunking (A2) follows functions.py:56-76.  GPU: the shim's
+landmark_extraction reproduces the reference run chunk by chunk on numpy's
+global RNG; System.ukf runs predict/update on the device."""
+import numpy as np
+import pytest
+
+from lidar_slam_amd import functions, landmarking, ransac_functions, systemClass
+
+
+def test_constants_mirror_reference():
+    assert (ransac_functions.THRESHOLD, ransac_functions.MAX_TRIALS, ransac_functions.MIN_SAMPLES) == (20, 100, 2)
+    assert (landmarking.LIFE, landmarking.TOLERANCE_A, landmarking.TOLERANCE_B, landmarking.TOLERANCE) == \
+        (40, 0.1, 10, 100)
+    assert systemClass.LANDMARK_NUMBER == 8 and systemClass.DT == 0.005
+    assert functions.MIN_NEIGHBOORS == 100
+
+
+def test_landmark_value_object():
+    L = landmarking.Landmark(0.5, 3.0, 7, 1.0, 2.0, 50.0, 28.0)
+    assert L.get_life() == 40 and L.get_id() == 7
+    for _ in range(39):
+        assert L.decrease_life() is None
+    assert L.decrease_life() is True and L.get_life() == 0
+    assert L.decrease_life() is True and L.get_life() == 0
+    L.reset_life()
+    assert L.get_life() == 40
+    M = landmarking.Landmark(0.55, 3.0, 8, 50.0, 28.0, 500.0, 250.0)
+    assert L.is_equal(M)  # ||pos_M - end_L|| = 0
+    M.a = 0.7
+    assert not L.is_equal(M)
+    lst = [L]
+    L.life = 0
+    landmarking.landmarks_track(lst)   # reference bug kept: never removes
+    assert lst == [L]
+
+
+def test_chunker_matches_functions_py():
+    class Q(list):
+        def put(self, x):
+            self.append(x)
+
+    q = Q()
+    ch = functions.ScanChunker(q, warmup_s=0.0, start_time=-1.0)
+    ch._emit = lambda: (q.put(len(ch.th)), ch.th.clear(), ch.d.clear())   # count instead of converting
+    for k in range(720):
+        ch.push(k == 719, k * 0.5, 1000.0, t=0.0)
+    # 7 chunks of 100; the flagged 720th measure joins the remainder (20 > 2); then the delimiter
+    assert q == [100] * 7 + [20, 0]
+    q.clear()
+    for k in range(701):
+        ch.push(k == 700, k * 0.5, 1000.0, t=0.0)
+    assert q == [100] * 7 + [0]      # remainder of 1 point is dropped (functions.py:71)
+    assert list(functions.chunk_offsets(720)) == [0, 100, 200, 300, 400, 500, 600, 700, 720]
+
+
+@pytest.mark.gpu
+def test_shim_replays_live_reference_run(golden):
+    """The live fixture (one global RNG stream, one landmark list, 112 chunks)
+    replayed through ransac_functions.landmark_extraction on numpy's global state."""
+    g = golden("live.npz")
+    np.random.seed(int(g["seed"][0]))
+    landmarks = []
+    number = 0
+    for c in range(len(g["a"])):
+        p0, p1 = g["chunk_pt_off"][c], g["chunk_pt_off"][c + 1]
+        pts = [g["xy"][p0:p1].tolist()]
+        q, fitted, new = ransac_functions.landmark_extraction(pts, number, landmarks)
+        assert pts == []
+        if new:
+            landmarks.append(fitted)
+        number += 1
+        st = np.random.get_state()
+        assert np.array_equal(st[1], g["state_after_key"][c]) and st[2] == g["state_after_pos"][c]
+        q0, q1 = g["q_off"][c], g["q_off"][c + 1]
+        assert [p.x() for p in q] == list(g["q_x"][q0:q1])
+        assert np.allclose([p.y() for p in q], g["q_y"][q0:q1], rtol=1e-9, atol=1e-9)
+        assert bool(new) == bool(g["new_landmark"][c])
+        l0, l1 = g["lm_off"][c], g["lm_off"][c + 1]
+        assert [L.id for L in landmarks] == list(g["lm_id"][l0:l1])
+        assert [L.life for L in landmarks] == list(g["lm_life"][l0:l1])
+
+
+@pytest.mark.gpu
+def test_shim_errors_match_reference():
+    np.random.seed(3)
+    with pytest.raises(ValueError):
+        ransac_functions.landmark_extraction([[[0.0, 0.0], [1.0, 1.0]]], 0, [])
+    st = np.random.get_state()
+    assert np.array_equal(st[1], np.random.RandomState(3).get_state()[1])  # nothing consumed
+
+
+@pytest.mark.gpu
+def test_system_ukf_vs_oracle():
+    from oracle import ukf as oukf
+    sysm = systemClass.System([])
+    sysm.ukf.x = np.array([1000.0, 800.0, 0.3])
+    rng = np.random.default_rng(2)
+    lm = [tuple(p) for p in rng.uniform(-3000, 3000, (8, 2))]
+    z = oukf.transfer_function(np.array([1000.0, 800.0, 0.3]), lm) + 0.05
+    sysm.ukf.predict(u=[2.0, 2.5])
+    sysm.ukf.update(z, landmarks=lm)
+    f = oukf.UKF(8)
+    f.x = np.array([1000.0, 800.0, 0.3])
+    f.predict(np.array([2.0, 2.5]))
+    f.update(z, lm)
+    assert np.max(np.abs(sysm.ukf.x - f.x)) < 1e-4
+    assert np.max(np.abs(sysm.ukf.P - f.P)) < 1e-6
