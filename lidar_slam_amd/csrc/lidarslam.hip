@@ -52,11 +52,12 @@ struct KArgs {
     int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg;
     int corg_cap;
     int off_ukf;
-    uint32_t ring_mask;
+    int off_j1;
     int pts_cap;
     int lmk_cap;
     int hist_cap;
     UkfConst ukf;
+    unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
 };
 
 // ------------------------------------------------------------------------
@@ -366,9 +367,12 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
 
     MTWave mt;
     mt.key = key;
-    mt.ring = (uint16_t *)(smem + a.off_ring);
-    mt.ring_mask = a.ring_mask;
+    mt.nxt = (uint32_t *)(smem + a.off_ring);
+    mt.j1s = (uint32_t *)(smem + a.off_j1);
     mt.pos = MT_N;
+#ifdef LSLAM_STAMPS
+    for (int k = 0; k < 8; k++) mt.acc[k] = 0;
+#endif
 
     auto mt_init = [&]() {
         if (B.mt_state_in) {
@@ -525,6 +529,10 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         __syncthreads();
     }
 
+#ifdef LSLAM_STAMPS
+    if (a.dbg && lane == 0)
+        for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 8 + k] = mt.acc[k];
+#endif
     if (use_mt && B.mt_state_out) {
         uint32_t *dst = B.mt_state_out + (size_t)s * 625;
         for (int i = lane; i < MT_N; i += 64) dst[i] = key[i];
@@ -880,14 +888,26 @@ static int validate_batch(const lslam_scan_batch *b, bool need_points) {
     return LSLAM_OK;
 }
 
+#ifdef LSLAM_STAMPS
+static unsigned long long *g_dbg = nullptr;
+extern "C" int lslam_debug_set_stamps(unsigned long long *dev_buf) {
+    g_dbg = dev_buf;
+    return LSLAM_OK;
+}
+#endif
+
 static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_params *p, const lslam_ukf_params *u,
                       int mode, int &lds) {
     memset(&k, 0, sizeof(k));
+#ifdef LSLAM_STAMPS
+    k.dbg = g_dbg;
+#endif
     k.b = *b;
     if (p) {
         if (p->min_samples != 2) return set_err(LSLAM_ERR_UNSUPPORTED, "only min_samples == 2 (ransac_functions.py:11)");
         if (p->residual_threshold < 0) return set_err(LSLAM_ERR_ARG, "`residual_threshold` must be greater than zero");
         if (p->max_trials < 0) return set_err(LSLAM_ERR_ARG, "`max_trials` must be greater than zero");
+        if (p->max_trials > 65533) return set_err(LSLAM_ERR_UNSUPPORTED, "max_trials > 65533");
         if (p->hyp_source < 0 || p->hyp_source > 2) return set_err(LSLAM_ERR_ARG, "bad hyp_source");
         if (p->hyp_source == LSLAM_HYP_EXPLICIT && !b->hyp) return set_err(LSLAM_ERR_ARG, "explicit hyp without hyp");
         k.thr = p->residual_threshold;
@@ -906,16 +926,16 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     int off = 0;
     k.off_pts = off; off += align16(16 * N);
     k.off_key = off; off += align16(4 * 624);
-    uint32_t ring = 64;
-    while (ring < (uint32_t)(N + 64)) ring <<= 1;
-    k.ring_mask = ring - 1;
-    // phase-exclusive scratch shares one region: the J ring (draw generation),
-    // then the tie sums (selection), then the inlier list (mask + refit)
-    const int uni_bytes = max(max(2 * (int)ring, 8 * (T > 0 ? T : 1)), 4 * N);
+    // phase-exclusive scratch shares one region: the draw-resolution tables
+    // (draw generation), then the tie sums (selection), then the inlier list
+    const int nxt_bytes = 4 * mt_nslot(N) * N;
+    const int uni_bytes = max(max(nxt_bytes, 8 * (T > 0 ? T : 1)), 4 * N);
     k.off_ring = off;
     k.off_tsum = off;
     k.off_inl = off;
     off += align16(uni_bytes);
+    k.off_j1 = off;
+    off += align16(4 * mt_nslot(N));
     k.off_draws = off; off += align16(8 * (T + 1));
     k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
