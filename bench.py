@@ -85,6 +85,35 @@ def cpu_baseline(n_scans, n_beams, L, procs):
     return done / dt, dt
 
 
+def shard_scan_ids(rank, per_rank):
+    """Weak scaling: rank r owns scans [r*per_rank, (r+1)*per_rank)."""
+    return list(range(rank * per_rank, (rank + 1) * per_rank))
+
+
+def timed_region(step, steps, warmup, sync, barrier):
+    """W untimed steps, then exactly K steps bracketed by barrier + sync."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def reduce_max(x, dist):
+    if dist is None:
+        return float(x)
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def load_traffic(path):
     try:
         with open(path) as f:
@@ -138,7 +167,7 @@ def main():
 
     ctx = Context(local)
     S = args.scans
-    ids = list(range(rank * S, (rank + 1) * S))
+    ids = shard_scan_ids(rank, S)
     b, ukf = make_workload(ids, args.beams, L, seed_base=rank)
     pipe = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
                         max_trials=args.trials, hyp=args.hyp, lmk_capacity=32, want_yproj=True,
@@ -160,31 +189,20 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
+    def step():
         pipe.run(sync=False)
+
+    # warmup outside the HIP-event window, then the timed region with events on
+    for _ in range(args.warmup):
+        step()
     sync_all()
     ctx.set_timing(True)
     ctx.timing_reset()
-    barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.run(sync=False)
-    sync_all()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(step, args.steps, 0, sync_all, barrier)
     kms, klaunch = ctx.timing(_lib.K_PIPELINE)
     ctx.set_timing(False)
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kms / max(klaunch, 1)], dtype=torch.float64)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kavg = float(k.item())
-    else:
-        kavg = kms / max(klaunch, 1)
+    elapsed = reduce_max(elapsed, dist)
+    kavg = reduce_max(kms / max(klaunch, 1), dist)
 
     # sanity: results are well-formed (every chunk fitted or flagged)
     r = pipe.results()

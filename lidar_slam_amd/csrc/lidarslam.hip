@@ -942,6 +942,13 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     k.off_mask = off; off += align16(N);
     k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
     k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+    // the UKF runs after the last chunk: its scratch aliases the RANSAC scratch
+    // above (offset 0); only the persistent region below (chunk history, chunk
+    // origins, landmark list) is live across both
+    if (u && u->n_landmarks > 0) {
+        k.off_ukf = 0;
+        off = max(off, align16(8 * UkfLds::doubles(u->n_landmarks)));
+    }
     k.hist_cap = b->max_scan_chunks > 0 ? b->max_scan_chunks : 1;
     k.off_hist = off; off += align16(4 * k.hist_cap);
     k.corg_cap = k.hist_cap;
@@ -966,8 +973,6 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         for (int i = 0; i < 9; i++) k.ukf.Q[i] = u->Q[i];
         k.ukf.L = u->n_landmarks;
         k.ukf.flags = u->flags;
-        k.off_ukf = off;
-        off += align16(8 * UkfLds::doubles(u->n_landmarks));
     }
     lds = off;
     if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk/trial/landmark sizes exceed the 160 KiB LDS");

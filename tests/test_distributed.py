@@ -1,0 +1,58 @@
+"""The multi-rank bench path on CPU (gloo, world_size 2, 127.0.0.1): scan
+sharding is a disjoint cover, the timed region is barrier-bracketed, and the
+elapsed time is the max over ranks.  The per-rank work here is the CPU oracle
+on each rank's shard, and the union of the shards' results equals the
+single-process run (the path has no exchange step, so none is tested)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    import bench
+    from lidar_slam_amd import synth
+    from oracle import cpu as orc
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = bench.shard_scan_ids(rank, 3)
+    b = synth.make_batch(ids)
+    res = {}
+
+    def step():
+        res["mask"] = orc.run_batch(b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], ids)[0]
+
+    el = bench.timed_region(step, 2, 1, lambda: None, dist.barrier)
+    # rank 1 pretends to be slower: the reported time must be the max
+    el_max = bench.reduce_max(el + (5.0 if rank == 1 else 0.0), dist)
+    out[rank] = (ids, res["mask"].tobytes(), el_max)
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sharding():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    ids0, m0, e0 = out[0]
+    ids1, m1, e1 = out[1]
+    assert set(ids0).isdisjoint(ids1) and sorted(ids0 + ids1) == list(range(6))
+    assert e0 == e1 and e0 >= 5.0
+    from lidar_slam_amd import synth
+    from oracle import cpu as orc
+    b = synth.make_batch(list(range(6)))
+    full = orc.run_batch(b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], list(range(6)))[0]
+    both = np.concatenate([np.frombuffer(m0, np.uint8), np.frombuffer(m1, np.uint8)])
+    assert np.array_equal(both, full)
