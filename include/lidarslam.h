@@ -179,7 +179,8 @@ int lslam_h2d(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* asy
 int lslam_d2h(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
 int lslam_memset(lslam_ctx *ctx, void *dst, int value, size_t bytes);     /* async */
 /* per-kernel HIP-event timing on the ctx stream (kernel ids: LSLAM_K_*) */
-enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMARK = 3, LSLAM_K_UKF = 4, LSLAM_K_COUNT = 5 };
+enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMARK = 3, LSLAM_K_UKF = 4,
+       LSLAM_K_RNG = 5 /* parity-stream producer */, LSLAM_K_CONSENSUS = 6 /* per-chunk A4-A8 */, LSLAM_K_COUNT = 7 };
 int lslam_set_timing(lslam_ctx *ctx, int enable);
 int lslam_timing(lslam_ctx *ctx, int kernel, double *total_ms, int64_t *launches);  /* syncs */
 int lslam_timing_reset(lslam_ctx *ctx);

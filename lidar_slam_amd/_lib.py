@@ -26,7 +26,7 @@ CAPACITY = 256
 
 HYP_MT19937, HYP_PHILOX, HYP_EXPLICIT = 0, 1, 2
 UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC = 1, 2, 4
-K_POLAR, K_HYP, K_PIPELINE, K_LANDMARK, K_UKF = 0, 1, 2, 3, 4
+K_POLAR, K_HYP, K_PIPELINE, K_LANDMARK, K_UKF, K_RNG, K_CONSENSUS = 0, 1, 2, 3, 4, 5, 6
 
 
 class HIPLibraryError(RuntimeError):

@@ -42,5 +42,15 @@ def build(force=False, verbose=True):
     return OUT
 
 
+def build_stamps():
+    """Diagnostic build with s_memtime phase stamps (tools/stamps.py)."""
+    out = os.path.join(HERE, "liblidarslam_stamps.so")
+    subprocess.check_call([HIPCC] + FLAGS + ["-DLSLAM_STAMPS", "-o", out, SRC])
+    return out
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--stamps" in sys.argv:
+        build_stamps()
+    else:
+        build(force="--force" in sys.argv)

@@ -2,13 +2,19 @@
 // Farofeiro231/LiDAR_SLAM.  See include/lidarslam.h for the reference entry
 // points each function replaces and DESIGN.md for the layout/roofline notes.
 //
-// Execution model: ONE wave (64 lanes) per scan, one scan per workgroup,
-// grid = n_scans.  Inside a scan the chunks are processed in order (the legacy
-// RNG stream is chained across them, ransac_functions.py:73 + fit.py:791):
-//   A3 draws -> A4/A5 counts (lane = hypothesis) -> A6 tie sums + selection
-//   -> mask + A7 refit -> A8 line params -> A9/A10 association -> (U1-U8 UKF)
-// Everything a scan touches lives in LDS/registers; HBM sees the points once
-// (16 B/point) and the outputs once.
+// Execution model (lslam_scan_pipeline, parity mode):
+//   rng_kernel     one workgroup (parser wave + helper wave) per scan: the
+//                  scan's chained legacy MT19937 stream (ransac_functions.py:73
+//                  + fit.py:791) -> every chunk's T+1 draws, assuming no early
+//                  stop (lslam_rng_pipe.h)
+//   chunk_kernel   one wave per chunk: A4/A5 counts (lane = hypothesis), A6 tie
+//                  sums + selection, mask + A7 refit, A8 line parameters
+//   scan_kernel    (fix-up) one wave per scan; exits at once unless one of its
+//                  chunks stopped early, then replays the scan sequentially
+//   scan_kernel    (post) one wave per scan: A9/A10 association walk over the
+//                  chunks in order, y_proj, then U1-U8 UKF
+// Philox / explicit hypotheses skip the producer and the fix-up.  A chunk's
+// points, draws and scratch live in LDS; HBM sees the points once per pass.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared.
 // -ffp-contract=off is REQUIRED: hipcc contracts a*b+c into v_fma_f64 by
@@ -24,6 +30,7 @@
 
 #include "../../include/lidarslam.h"
 #include "lslam_rng.h"
+#include "lslam_rng_pipe.h"
 #include "lslam_ransac.h"
 #include "lslam_ukf.h"
 #include "lslam_wave.h"
@@ -33,7 +40,7 @@ using namespace lslam;
 static_assert(sizeof(lslam_chunk_model) == 112, "chunk model ABI");
 static_assert(sizeof(lslam_landmark) == 56, "landmark ABI");
 
-enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8 };
+enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8, MODE_POST = 16 };
 
 // ------------------------------------------------------------------------
 // kernel arguments (passed by value)
@@ -57,6 +64,12 @@ struct KArgs {
     int lmk_cap;
     int hist_cap;
     UkfConst ukf;
+    // split pipeline
+    int32_t *hyp_scr;   // [n_chunks][T+1][2] draws from rng_kernel
+    uint32_t rjmask;    // rng_kernel: J ring size - 1
+    int off_blk, off_jr, off_fl, off_nxt;
+    int fixup;          // scan_kernel: only scans with an early-stopped chunk run
+    int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
 };
 
@@ -235,6 +248,35 @@ __device__ ChunkOut chunk_ransac(const KArgs &a, const double2 *P, int N, const 
     return o;
 }
 
+// mask (LDS copy + global) and A8 line parameters (ransac_functions.py:25-31)
+__device__ bool finish_chunk(const KArgs &a, const ChunkOut &o, const double2 *P, const int32_t *inl, uint8_t *mk,
+                             int p0, int N, lslam_chunk_model &rec, int lane) {
+    const lslam_scan_batch &B = a.b;
+    const bool valid = (o.flags & LSLAM_VALID) != 0;
+    for (int p = lane; p < N; p += 64) mk[p] = 0;
+    __syncthreads();
+    if (valid)
+        for (int k = lane; k < o.n_inl; k += 64) mk[inl[k]] = 1;
+    __syncthreads();
+    if (B.inlier_mask)
+        for (int p = lane; p < N; p += 64) B.inlier_mask[p0 + p] = mk[p];
+    rec.n_inliers = valid ? o.n_inl : 0;
+    rec.best_trial = o.best;
+    rec.n_draws = o.n_draws;
+    rec.flags = o.flags;
+    if (valid) {
+        const Model fm = o.m;
+        const double av = fm.uy / fm.ux;
+        const double bv = fm.oy - av * fm.ox;
+        const double tx = P[o.last_inl].x;
+        const double ty = tx * av + bv;
+        rec.ox = fm.ox; rec.oy = fm.oy; rec.ux = fm.ux; rec.uy = fm.uy;
+        rec.a = av; rec.b = bv; rec.tip_x = tx; rec.tip_y = ty;
+        rec.proj_a = av; rec.proj_b = bv;
+    }
+    return valid;
+}
+
 // ------------------------------------------------------------------------
 // landmark association (ransac_functions.py:34-54, landmarking.py:48-77)
 // list in LDS: lmk[0..L)
@@ -365,6 +407,17 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
     const int nchunks = c1 - c0;
     const int T = a.T;
 
+    constexpr bool kRansac = (MODE & (MODE_RANSAC | MODE_HYP_ONLY)) != 0;
+    constexpr bool use_mt = kRansac && HYP == LSLAM_HYP_MT19937;
+    constexpr bool kPost = !kRansac && (MODE & (MODE_ASSOC | MODE_POST)) != 0;
+    if (kRansac && a.fixup) {
+        // fix-up pass after rng_kernel + chunk_kernel: only a scan with an
+        // early-stopped chunk consumed a different stream; replay it whole
+        bool any = false;
+        for (int c = c0 + lane; c < c1; c += 64) any |= (B.models[c].flags & LSLAM_EARLY_STOP) != 0;
+        if (ballot(any) == 0ull) return;
+    }
+
     MTWave mt;
     mt.key = key;
     mt.nxt = (uint32_t *)(smem + a.off_ring);
@@ -386,8 +439,6 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         }
     };
 
-    constexpr bool kRansac = (MODE & (MODE_RANSAC | MODE_HYP_ONLY)) != 0;
-    constexpr bool use_mt = kRansac && HYP == LSLAM_HYP_MT19937;
     if (use_mt) mt_init();
 
     // landmark list of this scan -> LDS
@@ -403,7 +454,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
     }
     const int id0 = B.id_base ? B.id_base[s] : 0;
 
-    for (int ci = 0; ci < nchunks && (kRansac || (MODE & MODE_ASSOC)); ci++) {
+    for (int ci = 0; ci < nchunks && (kRansac || kPost); ci++) {
         const int c = c0 + ci;
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
@@ -469,37 +520,16 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
                     mt_draws(mt, (uint32_t)N, (uint32_t)o.n_draws, nullptr, false, lane);
                 }
             }
-            // ---- mask (LDS copy + global)
-            const bool valid = (o.flags & LSLAM_VALID) != 0;
-            for (int p = lane; p < N; p += 64) mk[p] = 0;
-            __syncthreads();
-            if (valid)
-                for (int k = lane; k < o.n_inl; k += 64) mk[inl[k]] = 1;
-            __syncthreads();
-            if (B.inlier_mask)
-                for (int p = lane; p < N; p += 64) B.inlier_mask[p0 + p] = mk[p];
-            // ---- A8 line parameters (ransac_functions.py:25-31)
-            rec.n_inliers = valid ? o.n_inl : 0;
-            rec.best_trial = o.best;
-            rec.n_draws = o.n_draws;
-            rec.flags = o.flags;
-            if (valid) {
-                have_model = true;
-                const Model fm = o.m;
-                const double av = fm.uy / fm.ux;
-                const double bv = fm.oy - av * fm.ox;
-                const double tx = P[o.last_inl].x;
-                const double ty = tx * av + bv;
-                rec.ox = fm.ox; rec.oy = fm.oy; rec.ux = fm.ux; rec.uy = fm.uy;
-                rec.a = av; rec.b = bv; rec.tip_x = tx; rec.tip_y = ty;
-                rec.proj_a = av; rec.proj_b = bv;
-                if (ci < a.corg_cap && lane == 0) corg[ci] = make_double2(fm.ox, fm.oy);
-            }
+            have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
+            if (have_model && ci < a.corg_cap && lane == 0) corg[ci] = make_double2(rec.ox, rec.oy);
         } else {
-            // association-only mode: models and masks come from a previous ransac launch
+            // post pass: models and masks come from a previous ransac launch
             rec = B.models[c];
             have_model = (rec.flags & LSLAM_VALID) != 0;
-            for (int p = lane; p < N; p += 64) mk[p] = B.inlier_mask[p0 + p];
+            if (ci < a.corg_cap && lane == 0)
+                corg[ci] = have_model ? make_double2(rec.ox, rec.oy) : make_double2(__builtin_nan(""), __builtin_nan(""));
+            if (MODE & MODE_ASSOC)
+                for (int p = lane; p < N; p += 64) mk[p] = B.inlier_mask[p0 + p];
             __syncthreads();
         }
 
@@ -518,14 +548,14 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
                 if (overflow) rec.flags |= LSLAM_CAPACITY;
             }
         }
-        if (B.y_proj) {
+        if (B.y_proj && (kRansac || (MODE & MODE_ASSOC))) {
             const double pa = rec.proj_a, pb = rec.proj_b;
             for (int p = lane; p < N; p += 64) {
                 const double x = B.xy[2 * (size_t)(p0 + p)];
                 B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
             }
         }
-        if (lane == 0 && B.models) B.models[c] = rec;
+        if (lane == 0 && B.models && (kRansac || (MODE & MODE_ASSOC))) B.models[c] = rec;
         __syncthreads();
     }
 
@@ -554,7 +584,7 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         u[1] = B.ukf_u[2 * (size_t)s + 1];
         const int Lu = a.ukf.L;
         const double *lm = B.ukf_lmk + (size_t)s * 2 * Lu;
-        const int nfuse = ((a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC) && (MODE & MODE_RANSAC))
+        const int nfuse = ((a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC) && (kRansac || kPost))
                               ? min(nchunks, a.corg_cap) : 0;
         auto lmk_fn = [&](int j, double &px, double &py) {
             px = lm[2 * j];
@@ -572,6 +602,199 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
             for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
         }
     }
+}
+
+// ------------------------------------------------------------------------
+// rng_kernel: the chained parity stream of one scan -> every chunk's draws
+// (wave 0 parses, wave 1 twists ahead and resolves; lslam_rng_pipe.h)
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int s = blockIdx.x;
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = uni((int)threadIdx.x >> 6);
+    const lslam_scan_batch &B = a.b;
+    RngPipe rp;
+    rp.raw = (uint32_t *)(smem + a.off_blk);
+    rp.tw = rp.raw + MT_N;
+    rp.jr = (uint16_t *)(smem + a.off_jr);
+    rp.nxt = (uint32_t *)(smem + a.off_nxt);
+    rp.fl = (lds_flag_t *)(smem + a.off_fl);
+    rp.rjmask = a.rjmask;
+#ifdef LSLAM_STAMPS
+    for (int k = 0; k < 8; k++) rp.acc[k] = 0;
+    const uint64_t t_start = lslam_stamp();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
+    const uint32_t D = (uint32_t)a.T + 1u;
+    int32_t *dst = a.hyp_scr;
+    if (wave == 1) {
+        if (B.mt_state_in) {
+            const uint32_t *src = B.mt_state_in + (size_t)s * 625;
+            for (int i = lane; i < MT_N; i += 64) rp.raw[i] = src[i];
+        } else {
+            mt_seed(rp.raw, B.seeds ? B.seeds[s] : 0u, lane);
+        }
+        wave_lds_sync();
+        for (int i = lane; i < MT_N; i += 64) rp.tw[i] = mt_temper(rp.raw[i]);
+        if (lane < F_NFLAGS) rp.fl[lane] = 0;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // ---- parser: its chain is the kernel's critical path
+        rp.ndrawn = 0;
+        int blkno = 0;
+        int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
+        uint32_t gs = 0;
+        int dres_seen = 0;
+        for (int c = c0; c < c1; c++) {
+            const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
+            if (N < 3) continue;
+            if (N >= 65) parse_chunk<true>(rp, blkno, pos, gs, dres_seen, (uint32_t)N, D, lane);
+            else parse_chunk<false>(rp, blkno, pos, gs, dres_seen, (uint32_t)N, D, lane);
+        }
+        wake_helper();
+        if (B.mt_state_out) {
+            uint32_t *o = B.mt_state_out + (size_t)s * 625;
+            const uint32_t *kb = rp.tw + (blkno & 1) * MT_N;
+            for (int i = lane; i < MT_N; i += 64) o[i] = mt_untemper(kb[i]);
+            if (lane == 0) o[624] = (uint32_t)pos;
+        }
+#ifdef LSLAM_STAMPS
+        rp.acc[7] = lslam_stamp() - t_start;
+        rp.acc[4] = rt_start;  // residency census (100 MHz chip-wide clock)
+        rp.acc[3] = __builtin_amdgcn_s_memrealtime();
+        if (a.dbg && lane == 0) {
+            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
+            // placement census: HW_ID simd / cu / se of the parser, xcc
+            a.dbg[(size_t)s * 16 + 8] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+            a.dbg[(size_t)s * 16 + 9] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (8 << 6) | (3 << 11));
+            a.dbg[(size_t)s * 16 + 10] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (13 << 6) | (2 << 11));
+            a.dbg[(size_t)s * 16 + 11] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+            a.dbg[(size_t)s * 16 + 13] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (12 << 6) | (0 << 11));
+        }
+#endif
+    } else {
+        // ---- helper: short bursts (twist, resolve), asleep otherwise
+        __builtin_amdgcn_s_setprio(1);
+#ifdef LSLAM_STAMPS
+        if (a.dbg && lane == 0)
+            a.dbg[(size_t)s * 16 + 12] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+#endif
+        int produced = 0;
+        int cc = c0;
+        auto chunk_n = [&](int c) { return B.chunk_pt_off[c + 1] - B.chunk_pt_off[c]; };
+        auto clear_nxt = [&](int n) {
+            for (int e = lane; e < n; e += 64) rp.nxt[e] = MT_NONE;
+            wave_lds_sync();
+        };
+        while (cc < c1 && chunk_n(cc) < 3) cc++;
+        uint32_t K = 2u;
+        if (cc < c1) {
+            K = (uint32_t)chunk_n(cc) - 1u;
+            clear_nxt((int)K + 1);
+        }
+        uint32_t base = 0, dnext = 0;
+        while (cc < c1) {
+            if (lds_flag_get(rp.fl + F_BLKUSE) == produced) {
+                mt_twist(rp.raw, lane);
+                uint32_t *dstb = rp.tw + ((produced + 1) & 1) * MT_N;
+                for (int i = lane; i < MT_N; i += 64) dstb[i] = mt_temper(rp.raw[i]);
+                produced += 1;
+                lds_flag_put(rp.fl + F_BLK, produced, lane);
+                continue;
+            }
+            const int avail = lds_flag_get(rp.fl + F_GPAR) - (int)base;
+            const uint32_t complete = avail > 0 ? min(D, (uint32_t)avail / K) : 0u;
+            if (complete <= dnext) {
+                __builtin_amdgcn_s_sleep(127);  // until the parser's s_wakeup
+                continue;
+            }
+            int32_t *out = dst + (size_t)cc * 2 * D;
+            for (; dnext < complete; dnext++) resolve_draw(rp, base + dnext * K, K, dnext, out, lane);
+            if (dnext == D) {
+                base += D * K;
+                dnext = 0;
+                cc++;
+                while (cc < c1 && chunk_n(cc) < 3) cc++;
+                if (cc < c1) {
+                    K = (uint32_t)chunk_n(cc) - 1u;
+                    clear_nxt((int)K + 1);
+                }
+            }
+            lds_flag_put(rp.fl + F_DRES, (int)(base + dnext * K), lane);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// chunk_kernel: one wave per chunk, A4-A8 with the draws given
+// ------------------------------------------------------------------------
+template <int HYP>
+__global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int c = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    double2 *P = (double2 *)(smem + a.off_pts);
+    int32_t *draws = (int32_t *)(smem + a.off_draws);
+    int32_t *cnt = (int32_t *)(smem + a.off_cnt);
+    int32_t *tied = (int32_t *)(smem + a.off_tied);
+    double *tsum = (double *)(smem + a.off_tsum);
+    int32_t *inl = (int32_t *)(smem + a.off_inl);
+    uint8_t *mk = (uint8_t *)(smem + a.off_mask);
+    double *vstack = (double *)(smem + a.off_vstack);
+    int *nstack = (int *)(smem + a.off_nstack);
+
+    // owning scan: the last s with scan_chunk_off[s] <= c
+    int lo = 0, hi = B.n_scans;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (B.scan_chunk_off[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    const int s = uni(lo);
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    const int T = a.T;
+    lslam_chunk_model rec;
+    memset(&rec, 0, sizeof(rec));
+    rec.best_trial = -1;
+    rec.match_index = -1;
+    rec.landmark_id = (B.id_base ? B.id_base[s] : 0) + (c - B.scan_chunk_off[s]);
+    rec.n_points = N;
+    if (N < 3) {
+        rec.flags = LSLAM_N_TOO_SMALL;
+        if (lane == 0 && B.models) B.models[c] = rec;
+        for (int p = lane; p < N; p += 64) {
+            if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
+            if (B.y_proj && a.write_yproj) B.y_proj[p0 + p] = 0.0;
+        }
+        return;
+    }
+    const int D = T + 1;
+    if (HYP == LSLAM_HYP_PHILOX) {
+        philox_draws((uint32_t)N, (uint32_t)D, (uint32_t)c, a.philox_seed, draws, lane);
+        if (B.draws_out)
+            for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
+    } else {
+        const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.hyp_scr) + (size_t)c * 2 * D;
+        for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
+        if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
+            for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
+    }
+    const double2 *src = (const double2 *)B.xy + p0;
+    for (int p = lane; p < N; p += 64) P[p] = src[p];
+    __syncthreads();
+    const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack,
+                                    B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
+    const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
+    if (B.y_proj && a.write_yproj) {
+        const double pa = rec.proj_a, pb = rec.proj_b;
+        for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
+    }
+    if (lane == 0 && B.models) B.models[c] = rec;
 }
 
 // A1: polar -> Cartesian (functions.py:59-60)
@@ -601,6 +824,9 @@ struct lslam_ctx {
     int head[LSLAM_K_COUNT], npend[LSLAM_K_COUNT];
     double total_ms[LSLAM_K_COUNT];
     int64_t launches[LSLAM_K_COUNT];
+    // draws handed from rng_kernel to chunk_kernel when the caller gives no draws_out
+    void *scr;
+    size_t scr_bytes;
 };
 
 static thread_local std::string g_err;
@@ -657,6 +883,8 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     if (!c) return LSLAM_ERR_NOMEM;
     c->device = device;
     c->timing = false;
+    c->scr = nullptr;
+    c->scr_bytes = 0;
     for (int k = 0; k < LSLAM_K_COUNT; k++) {
         c->total_ms[k] = 0;
         c->launches[k] = 0;
@@ -687,6 +915,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
             if (c->ev0[k][r]) (void)hipEventDestroy(c->ev0[k][r]);
             if (c->ev1[k][r]) (void)hipEventDestroy(c->ev1[k][r]);
         }
+    if (c->scr) (void)hipFree(c->scr);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -924,24 +1153,29 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
     const int T = k.T;
     int off = 0;
-    k.off_pts = off; off += align16(16 * N);
-    k.off_key = off; off += align16(4 * 624);
-    // phase-exclusive scratch shares one region: the draw-resolution tables
-    // (draw generation), then the tie sums (selection), then the inlier list
-    const int nxt_bytes = 4 * mt_nslot(N) * N;
-    const int uni_bytes = max(max(nxt_bytes, 8 * (T > 0 ? T : 1)), 4 * N);
-    k.off_ring = off;
-    k.off_tsum = off;
-    k.off_inl = off;
-    off += align16(uni_bytes);
-    k.off_j1 = off;
-    off += align16(4 * mt_nslot(N));
-    k.off_draws = off; off += align16(8 * (T + 1));
-    k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
-    k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
-    k.off_mask = off; off += align16(N);
-    k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
-    k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+    if (mode & (MODE_RANSAC | MODE_HYP_ONLY)) {
+        k.off_pts = off; off += align16(16 * N);
+        k.off_key = off; off += align16(4 * 624);
+        // phase-exclusive scratch shares one region: the draw-resolution tables
+        // (draw generation), then the tie sums (selection), then the inlier list
+        const int nxt_bytes = 4 * mt_nslot(N) * N;
+        const int uni_bytes = max(max(nxt_bytes, 8 * (T > 0 ? T : 1)), 4 * N);
+        k.off_ring = off;
+        k.off_tsum = off;
+        k.off_inl = off;
+        off += align16(uni_bytes);
+        k.off_j1 = off;
+        off += align16(4 * mt_nslot(N));
+        k.off_draws = off; off += align16(8 * (T + 1));
+        k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
+        k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
+        k.off_mask = off; off += align16(N);
+        k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
+        k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+    } else {
+        // post pass (association / UKF over fitted models): only the chunk's mask
+        k.off_mask = off; off += align16(N);
+    }
     // the UKF runs after the last chunk: its scratch aliases the RANSAC scratch
     // above (offset 0); only the persistent region below (chunk history, chunk
     // origins, landmark list) is live across both
@@ -1015,6 +1249,166 @@ static int run_scan_kernel(lslam_ctx *c, const KArgs &k, int lds, int timer) {
     return LSLAM_OK;
 }
 
+
+// chunk_kernel LDS: one chunk's points, draws and consensus scratch
+static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
+    const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
+    const int T = k.T;
+    int off = 0;
+    k.off_pts = off; off += align16(16 * N);
+    k.off_draws = off; off += align16(8 * (T + 1));
+    k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
+    k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
+    k.off_tsum = off;  // tie sums, then the inlier list
+    k.off_inl = off;
+    off += align16(max(8 * (T > 0 ? T : 1), 4 * N));
+    k.off_mask = off; off += align16(N);
+    k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
+    k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+    lds = off;
+    if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk/trial sizes exceed the 160 KiB LDS");
+    return LSLAM_OK;
+}
+
+// rng_kernel LDS: raw MT block, two tempered blocks, the J ring (>= 2K + 128 steps), flags
+static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
+    const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
+    if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
+    const int64_t steps = (int64_t)(b->max_scan_chunks > 0 ? b->max_scan_chunks : 1) * (k.T + 1) * (N - 1);
+    if (steps >= (1ll << 30)) return set_err(LSLAM_ERR_UNSUPPORTED, "too many Fisher-Yates steps per scan");
+    int rj = 512;
+    while (rj < 2 * (N - 1) + 128) rj <<= 1;
+    k.rjmask = (uint32_t)rj - 1u;
+    int off = 0;
+    k.off_blk = off; off += align16(3 * 4 * 624);  // raw block + two tempered slots
+    k.off_jr = off; off += align16(2 * rj + 2 * 64);  // ring + one dummy slot per lane
+    k.off_nxt = off; off += align16(4 * N);
+    k.off_fl = off; off += align16(4 * F_NFLAGS);
+    lds = off;
+    if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk size exceeds the 160 KiB LDS");
+    return LSLAM_OK;
+}
+
+static int ensure_scratch(lslam_ctx *c, size_t bytes) {
+    if (c->scr_bytes >= bytes) return LSLAM_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->scr) HIPCHK(hipFree(c->scr));
+    c->scr = nullptr;
+    c->scr_bytes = 0;
+    hipError_t e = hipMalloc(&c->scr, bytes);
+    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (draw scratch)");
+    HIPCHK(e);
+    c->scr_bytes = bytes;
+    return LSLAM_OK;
+}
+
+template <typename F>
+static void set_max_lds(F *fn) {
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+static int launch_rng(lslam_ctx *c, const KArgs &base) {
+    KArgs k = base;
+    int lds = 0;
+    int st = layout_rng(k, &k.b, lds);
+    if (st) return st;
+    static std::once_flag once;
+    std::call_once(once, [] { set_max_lds(rng_kernel); });
+    st = timer_begin(c, LSLAM_K_RNG);
+    if (st) return st;
+    hipLaunchKernelGGL(rng_kernel, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
+    HIPCHK(hipGetLastError());
+    return timer_end(c, LSLAM_K_RNG);
+}
+
+static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
+    if (base.b.n_chunks == 0) return LSLAM_OK;
+    KArgs k = base;
+    k.write_yproj = write_yproj ? 1 : 0;
+    int lds = 0;
+    int st = layout_chunk(k, &k.b, lds);
+    if (st) return st;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        set_max_lds(chunk_kernel<LSLAM_HYP_MT19937>);
+        set_max_lds(chunk_kernel<LSLAM_HYP_PHILOX>);
+        set_max_lds(chunk_kernel<LSLAM_HYP_EXPLICIT>);
+    });
+    st = timer_begin(c, LSLAM_K_CONSENSUS);
+    if (st) return st;
+    const dim3 grid((unsigned)k.b.n_chunks), block(64);
+    switch (k.hyp_source) {
+        case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_PHILOX>, grid, block, lds, c->stream, k); break;
+        case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds, c->stream, k); break;
+        default: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_MT19937>, grid, block, lds, c->stream, k); break;
+    }
+    HIPCHK(hipGetLastError());
+    return timer_end(c, LSLAM_K_CONSENSUS);
+}
+
+template <int MODE>
+static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
+    static std::once_flag once;
+    std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>); });
+    hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), dim3((unsigned)k.b.n_scans), dim3(64), lds, c->stream, k);
+    HIPCHK(hipGetLastError());
+    return LSLAM_OK;
+}
+
+// rng_kernel -> chunk_kernel -> fix-up -> association/UKF post pass, all on the ctx stream
+static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p,
+                     const lslam_ukf_params *u) {
+    HIPCHK(hipSetDevice(c->device));
+    if (b->n_scans == 0) return LSLAM_OK;
+    const bool assoc = b->landmarks != nullptr;
+    KArgs k;
+    int lds_fix = 0;
+    int st = build_args(k, b, p, nullptr, MODE_RANSAC, lds_fix);
+    if (st) return st;
+    const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
+    if (mt) {
+        if (b->draws_out) {
+            k.hyp_scr = b->draws_out;
+        } else {
+            st = ensure_scratch(c, (size_t)(b->n_chunks > 0 ? b->n_chunks : 1) * 2 * (k.T + 1) * sizeof(int32_t));
+            if (st) return st;
+            k.hyp_scr = (int32_t *)c->scr;
+        }
+    }
+    KArgs kp;
+    int lds_post = 0;
+    const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u ? MODE_UKF : 0);
+    if (assoc || u) {
+        st = build_args(kp, b, p, u, pmode, lds_post);
+        if (st) return st;
+    }
+    st = timer_begin(c, LSLAM_K_PIPELINE);
+    if (st) return st;
+    if (mt) {
+        st = launch_rng(c, k);
+        if (st) return st;
+    }
+    st = launch_chunks(c, k, !assoc);
+    if (st) return st;
+    if (mt) {
+        KArgs kf = k;
+        kf.fixup = 1;
+        static std::once_flag once;
+        std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>); });
+        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3((unsigned)b->n_scans), dim3(64), lds_fix,
+                           c->stream, kf);
+        HIPCHK(hipGetLastError());
+    }
+    switch (pmode) {
+        case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post); break;
+        case MODE_POST | MODE_UKF: st = launch_post<MODE_POST | MODE_UKF>(c, kp, lds_post); break;
+        case MODE_ASSOC: st = launch_post<MODE_ASSOC>(c, kp, lds_post); break;
+        default: break;
+    }
+    if (st) return st;
+    return timer_end(c, LSLAM_K_PIPELINE);
+}
+
 extern "C" {
 
 int lslam_polar_to_xy(lslam_ctx *c, const double *th, const double *d, double *xy, int64_t n) {
@@ -1044,18 +1438,21 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     int lds = 0;
     st = build_args(k, b, &p, nullptr, MODE_HYP_ONLY, lds);
     if (st) return st;
-    return run_scan_kernel<MODE_HYP_ONLY>(c, k, lds, LSLAM_K_HYP);
+    HIPCHK(hipSetDevice(c->device));
+    if (b->n_scans == 0) return LSLAM_OK;
+    k.hyp_scr = b->draws_out;
+    st = timer_begin(c, LSLAM_K_HYP);
+    if (st) return st;
+    st = launch_rng(c, k);
+    if (st) return st;
+    return timer_end(c, LSLAM_K_HYP);
 }
 
 int lslam_ransac(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p) {
     if (!c || !p) return LSLAM_ERR_ARG;
     int st = validate_batch(b, true);
     if (st) return st;
-    KArgs k;
-    int lds = 0;
-    st = build_args(k, b, p, nullptr, MODE_RANSAC, lds);
-    if (st) return st;
-    return run_scan_kernel<MODE_RANSAC>(c, k, lds, LSLAM_K_PIPELINE);
+    return run_split(c, b, p, nullptr);
 }
 
 int lslam_landmarks(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p) {
@@ -1088,19 +1485,7 @@ int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ran
     if (!c || !p) return LSLAM_ERR_ARG;
     int st = validate_batch(b, true);
     if (st) return st;
-    KArgs k;
-    int lds = 0;
-    const bool assoc = b->landmarks != nullptr;
-    const int mode = MODE_RANSAC | (assoc ? MODE_ASSOC : 0) | (u ? MODE_UKF : 0);
-    st = build_args(k, b, p, u, mode, lds);
-    if (st) return st;
-    switch (mode) {
-        case MODE_RANSAC | MODE_ASSOC | MODE_UKF:
-            return run_scan_kernel<MODE_RANSAC | MODE_ASSOC | MODE_UKF>(c, k, lds, LSLAM_K_PIPELINE);
-        case MODE_RANSAC | MODE_UKF: return run_scan_kernel<MODE_RANSAC | MODE_UKF>(c, k, lds, LSLAM_K_PIPELINE);
-        case MODE_RANSAC | MODE_ASSOC: return run_scan_kernel<MODE_RANSAC | MODE_ASSOC>(c, k, lds, LSLAM_K_PIPELINE);
-        default: return run_scan_kernel<MODE_RANSAC>(c, k, lds, LSLAM_K_PIPELINE);
-    }
+    return run_split(c, b, p, u);
 }
 
 }  // extern "C"

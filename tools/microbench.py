@@ -21,7 +21,10 @@ from lidar_slam_amd import pipeline as pl  # noqa: E402
 from lidar_slam_amd.device import Context  # noqa: E402
 
 
-def timed(ctx, fn, kid, reps):
+BREAKDOWN = {}
+
+
+def timed(ctx, fn, kid, reps, tag=None):
     fn()
     ctx.sync()
     ctx.set_timing(True)
@@ -30,6 +33,11 @@ def timed(ctx, fn, kid, reps):
         fn()
     ctx.sync()
     ms, n = ctx.timing(kid)
+    if tag:
+        for name, k in (("rng", _lib.K_RNG), ("consensus", _lib.K_CONSENSUS)):
+            m2, n2 = ctx.timing(k)
+            if n2:
+                BREAKDOWN["%s_%s_ms" % (tag, name)] = m2 / n2
     ctx.set_timing(False)
     return ms / max(n, 1)
 
@@ -48,8 +56,8 @@ def main():
         for with_ukf in (True, False):
             p = pl.ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids), hyp=hyp,
                                 lmk_capacity=32, ukf=ukf if with_ukf else None)
-            res["pipeline_%s%s_ms" % (hyp, "_ukf" if with_ukf else "")] = timed(
-                ctx, lambda: p.run(sync=False), _lib.K_PIPELINE, args.reps)
+            tag = "pipeline_%s%s" % (hyp, "_ukf" if with_ukf else "")
+            res[tag + "_ms"] = timed(ctx, lambda: p.run(sync=False), _lib.K_PIPELINE, args.reps, tag)
         p = pl.ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids), hyp=hyp)
         res["ransac_only_%s_ms" % hyp] = timed(ctx, lambda: p.run_ransac_only(sync=False), _lib.K_PIPELINE, args.reps)
     p = pl.ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids), ukf=ukf)
@@ -72,6 +80,7 @@ def main():
     bb.draws_out = dr.addr
     res["mt19937_draws_only_ms"] = timed(
         ctx, lambda: _lib.check(_lib.load().lslam_hyp_mt19937(ctx.handle, C.byref(bb), 100)), _lib.K_HYP, args.reps)
+    res.update(BREAKDOWN)
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}))
 
 
