@@ -608,19 +608,20 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
 // rng_kernel: the chained parity stream of one scan -> every chunk's draws
 // (wave 0 parses, wave 1 twists ahead and resolves; lslam_rng_pipe.h)
 // ------------------------------------------------------------------------
+template <typename JT>
 __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int s = blockIdx.x;
     const int lane = (int)threadIdx.x & 63;
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
-    RngPipe rp;
-    rp.raw = (uint32_t *)(smem + a.off_blk);
-    rp.tw = rp.raw + MT_N;
-    rp.jr = (uint16_t *)(smem + a.off_jr);
+    RngPipe<JT> rp;
+    rp.blk = (uint32_t *)(smem + a.off_blk);
+    rp.jr = (JT *)(smem + a.off_jr);
     rp.nxt = (uint32_t *)(smem + a.off_nxt);
     rp.fl = (lds_flag_t *)(smem + a.off_fl);
     rp.rjmask = a.rjmask;
+    rp.nstride = (uint32_t)a.pts_cap;
 #ifdef LSLAM_STAMPS
     for (int k = 0; k < 8; k++) rp.acc[k] = 0;
     const uint64_t t_start = lslam_stamp();
@@ -628,22 +629,27 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
 #endif
     const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
     const uint32_t D = (uint32_t)a.T + 1u;
-    int32_t *dst = a.hyp_scr;
     if (wave == 1) {
+        // block 0 = the initial state (raw)
         if (B.mt_state_in) {
             const uint32_t *src = B.mt_state_in + (size_t)s * 625;
-            for (int i = lane; i < MT_N; i += 64) rp.raw[i] = src[i];
+            for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
         } else {
-            mt_seed(rp.raw, B.seeds ? B.seeds[s] : 0u, lane);
+            mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
         }
-        wave_lds_sync();
-        for (int i = lane; i < MT_N; i += 64) rp.tw[i] = mt_temper(rp.raw[i]);
         if (lane < F_NFLAGS) rp.fl[lane] = 0;
     }
     __syncthreads();
     if (wave == 0) {
         // ---- parser: its chain is the kernel's critical path
         rp.ndrawn = 0;
+        rp.total_steps = 0;
+        for (int c = c0; c < c1; c++) {
+            const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
+            if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
+        }
+        rp.prio = 2;
+        set_prio_level(2);
         int blkno = 0;
         int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
         uint32_t gs = 0;
@@ -657,8 +663,8 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
         wake_helper();
         if (B.mt_state_out) {
             uint32_t *o = B.mt_state_out + (size_t)s * 625;
-            const uint32_t *kb = rp.tw + (blkno & 1) * MT_N;
-            for (int i = lane; i < MT_N; i += 64) o[i] = mt_untemper(kb[i]);
+            const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
+            for (int i = lane; i < MT_N; i += 64) o[i] = kb[i];
             if (lane == 0) o[624] = (uint32_t)pos;
         }
 #ifdef LSLAM_STAMPS
@@ -677,54 +683,12 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
 #endif
     } else {
         // ---- helper: short bursts (twist, resolve), asleep otherwise
-        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(3);
 #ifdef LSLAM_STAMPS
         if (a.dbg && lane == 0)
             a.dbg[(size_t)s * 16 + 12] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
 #endif
-        int produced = 0;
-        int cc = c0;
-        auto chunk_n = [&](int c) { return B.chunk_pt_off[c + 1] - B.chunk_pt_off[c]; };
-        auto clear_nxt = [&](int n) {
-            for (int e = lane; e < n; e += 64) rp.nxt[e] = MT_NONE;
-            wave_lds_sync();
-        };
-        while (cc < c1 && chunk_n(cc) < 3) cc++;
-        uint32_t K = 2u;
-        if (cc < c1) {
-            K = (uint32_t)chunk_n(cc) - 1u;
-            clear_nxt((int)K + 1);
-        }
-        uint32_t base = 0, dnext = 0;
-        while (cc < c1) {
-            if (lds_flag_get(rp.fl + F_BLKUSE) == produced) {
-                mt_twist(rp.raw, lane);
-                uint32_t *dstb = rp.tw + ((produced + 1) & 1) * MT_N;
-                for (int i = lane; i < MT_N; i += 64) dstb[i] = mt_temper(rp.raw[i]);
-                produced += 1;
-                lds_flag_put(rp.fl + F_BLK, produced, lane);
-                continue;
-            }
-            const int avail = lds_flag_get(rp.fl + F_GPAR) - (int)base;
-            const uint32_t complete = avail > 0 ? min(D, (uint32_t)avail / K) : 0u;
-            if (complete <= dnext) {
-                __builtin_amdgcn_s_sleep(127);  // until the parser's s_wakeup
-                continue;
-            }
-            int32_t *out = dst + (size_t)cc * 2 * D;
-            for (; dnext < complete; dnext++) resolve_draw(rp, base + dnext * K, K, dnext, out, lane);
-            if (dnext == D) {
-                base += D * K;
-                dnext = 0;
-                cc++;
-                while (cc < c1 && chunk_n(cc) < 3) cc++;
-                if (cc < c1) {
-                    K = (uint32_t)chunk_n(cc) - 1u;
-                    clear_nxt((int)K + 1);
-                }
-            }
-            lds_flag_put(rp.fl + F_DRES, (int)(base + dnext * K), lane);
-        }
+        rng_helper(rp, B, c0, c1, D, a.hyp_scr, lane);
     }
 }
 
@@ -1270,19 +1234,22 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     return LSLAM_OK;
 }
 
-// rng_kernel LDS: raw MT block, two tempered blocks, the J ring (>= 2K + 128 steps), flags
-static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
+// rng_kernel LDS: two raw MT blocks, the J ring (>= 2K + 128 steps, u8 when
+// every chunk has <= 256 points) + 64 dummy slots, RES_NB next-writer tables, flags
+static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, bool &j8) {
     const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
     const int64_t steps = (int64_t)(b->max_scan_chunks > 0 ? b->max_scan_chunks : 1) * (k.T + 1) * (N - 1);
     if (steps >= (1ll << 30)) return set_err(LSLAM_ERR_UNSUPPORTED, "too many Fisher-Yates steps per scan");
+    j8 = N <= 256;
     int rj = 512;
     while (rj < 2 * (N - 1) + 128) rj <<= 1;
     k.rjmask = (uint32_t)rj - 1u;
+    k.pts_cap = N;  // next-writer table stride
     int off = 0;
-    k.off_blk = off; off += align16(3 * 4 * 624);  // raw block + two tempered slots
-    k.off_jr = off; off += align16(2 * rj + 2 * 64);  // ring + one dummy slot per lane
-    k.off_nxt = off; off += align16(4 * N);
+    k.off_blk = off; off += align16(2 * 4 * 624);
+    k.off_jr = off; off += align16((j8 ? 1 : 2) * (rj + 64));
+    k.off_nxt = off; off += align16(4 * RES_NB * N);
     k.off_fl = off; off += align16(4 * F_NFLAGS);
     lds = off;
     if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk size exceeds the 160 KiB LDS");
@@ -1310,13 +1277,18 @@ static void set_max_lds(F *fn) {
 static int launch_rng(lslam_ctx *c, const KArgs &base) {
     KArgs k = base;
     int lds = 0;
-    int st = layout_rng(k, &k.b, lds);
+    bool j8 = true;
+    int st = layout_rng(k, &k.b, lds, j8);
     if (st) return st;
     static std::once_flag once;
-    std::call_once(once, [] { set_max_lds(rng_kernel); });
+    std::call_once(once, [] {
+        set_max_lds(rng_kernel<uint8_t>);
+        set_max_lds(rng_kernel<uint16_t>);
+    });
     st = timer_begin(c, LSLAM_K_RNG);
     if (st) return st;
-    hipLaunchKernelGGL(rng_kernel, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
+    if (j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
+    else hipLaunchKernelGGL(rng_kernel<uint16_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
     HIPCHK(hipGetLastError());
     return timer_end(c, LSLAM_K_RNG);
 }
