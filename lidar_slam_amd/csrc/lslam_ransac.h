@@ -18,6 +18,12 @@
 
 namespace lslam {
 
+// single-wave workgroups: LDS ordering across lanes needs only a compiler barrier
+__device__ __forceinline__ void wave_lds_sync_rt() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 struct Model {
     double ox, oy, ux, uy;
 };
@@ -133,6 +139,93 @@ __device__ __forceinline__ void tls_direction(double sxx, double sxy, double syy
     if (!(nv > 0.0)) { ux = 1.0; uy = 0.0; return; }
     ux = vx / nv;
     uy = vy / nv;
+}
+
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Final refit on the inliers inl[0..nin) (data order), nin >= 3 (fit.py:84-95).
+// The mean is numpy's axis-0 add.reduce: sequential, done by every lane.  The
+// scatter matrix for the closed-form direction is our own quantity: inlier k
+// goes to lane k % 64 (ascending k), then an xor butterfly (32, 16, ..., 1)
+// leaves the same sums in every lane.  oracle/ransac_oracle.c:scatter2
+// restates this order.
+__device__ __forceinline__ Model refit_line(const double2 *P, const int32_t *inl, int nin, int lane) {
+    Model f;
+    double sx, sy;
+    {
+        const double2 q = P[inl[0]];
+        sx = q.x;
+        sy = q.y;
+    }
+    int i = 1;
+    for (; i + 4 <= nin; i += 4) {
+        const double2 q0 = P[inl[i]], q1 = P[inl[i + 1]], q2 = P[inl[i + 2]], q3 = P[inl[i + 3]];
+        sx += q0.x; sy += q0.y;
+        sx += q1.x; sy += q1.y;
+        sx += q2.x; sy += q2.y;
+        sx += q3.x; sy += q3.y;
+    }
+    for (; i < nin; i++) {
+        const double2 q = P[inl[i]];
+        sx += q.x;
+        sy += q.y;
+    }
+    f.ox = sx / (double)nin;
+    f.oy = sy / (double)nin;
+    double sxx = 0.0, sxy = 0.0, syy = 0.0;
+    for (int k = lane; k < nin; k += 64) {
+        const double2 q = P[inl[k]];
+        const double cx = q.x - f.ox, cy = q.y - f.oy;
+        sxx += cx * cx;
+        sxy += cx * cy;
+        syy += cy * cy;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sxx += __shfl_xor(sxx, o);
+        sxy += __shfl_xor(sxy, o);
+        syy += __shfl_xor(syy, o);
+    }
+    tls_direction(sxx, sxy, syy, f.ux, f.uy);
+    return f;
+}
+
+// numpy pairwise_sum of RN(sqrt(r^2))^2 over P[0..N), N <= 128, lanes over
+// points (pw_leaf's order): v_i by lane i % 64 into vtmp, accumulators
+// r_j = v_j + v_{j+8} + ... (lane j < 8, sequential), the fixed tree
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by xor shuffles, then the tail.
+__device__ __forceinline__ double pw_sum_lanes(const double2 *P, int N, const Model &m, double *vtmp, int lane) {
+    wave_lds_sync_rt();
+    if (lane < N) vtmp[lane] = r2sq(P[lane], m);
+    if (lane + 64 < N) vtmp[lane + 64] = r2sq(P[lane + 64], m);
+    wave_lds_sync_rt();
+    double res;
+    if (N < 8) {
+        res = 0.0;
+        for (int i = 0; i < N; i++) res += vtmp[i];
+        return res;
+    }
+    const int lim = N - (N % 8);
+    double r = 0.0;
+    if (lane < 8) {
+        r = vtmp[lane];
+        for (int i = lane + 8; i < lim; i += 8) r += vtmp[i];
+    }
+    r += __shfl_xor(r, 1);
+    r += __shfl_xor(r, 2);
+    r += __shfl_xor(r, 4);
+    res = unid(r);
+    for (int i = lim; i < N; i++) res += vtmp[i];
+    return res;
 }
 
 }  // namespace lslam

@@ -26,7 +26,8 @@
  *     fma(dx,ux, dy*uy); `np.linalg.norm(v)` as sqrt(fma(vy,vy, vx*vx));
  *     einsum('ij,ij->i') as plain rx*rx + ry*ry.
  *   - LAPACK dgesdd (final TLS refit, fit.py:94) is replaced by the closed-form
- *     principal eigenvector of the 2x2 scatter matrix (tls_direction below),
+ *     principal eigenvector of the 2x2 scatter matrix (tls_direction below,
+ *     scatter matrix summed in the kernel's lane order, scatter2),
  *     the SAME formula the HIP kernel uses; vs LAPACK it agrees to ~1e-14
  *     relative (checked against the golden vectors), with the sign of the
  *     direction normalised by nothing (a, b are sign-invariant).
@@ -182,6 +183,33 @@ typedef struct {
  * mask[n] out.  draws_out[(T+1)*2] optional.  cnt_out[T]/sum_out[T] optional
  * (sums only for trials whose count equals the maximum; others NaN).
  */
+/* Scatter matrix of the centred inliers for tls_direction, in the HIP
+ * kernel's order (lslam_ransac.h:refit_line): inlier k (data order) is added
+ * into partial sum k % 64 in ascending k, then the 64 partials are combined by
+ * an xor butterfly with offsets 32, 16, ..., 1 (every lane ends with the same
+ * value; lane 0's is returned). */
+static void scatter2(const double *xy, const uint8_t *mask, int32_t n, double ox, double oy,
+                     double *sxx_o, double *sxy_o, double *syy_o) {
+    double sxx[64], sxy[64], syy[64], t0[64], t1[64], t2[64];
+    for (int l = 0; l < 64; l++) sxx[l] = sxy[l] = syy[l] = 0.0;
+    int32_t k = 0;
+    for (int32_t p = 0; p < n; p++) if (mask[p]) {
+        double cx = xy[2 * p] - ox, cy = xy[2 * p + 1] - oy;
+        int l = k % 64;
+        sxx[l] += cx * cx; sxy[l] += cx * cy; syy[l] += cy * cy;
+        k++;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        for (int l = 0; l < 64; l++) {
+            t0[l] = sxx[l] + sxx[l ^ off];
+            t1[l] = sxy[l] + sxy[l ^ off];
+            t2[l] = syy[l] + syy[l ^ off];
+        }
+        for (int l = 0; l < 64; l++) { sxx[l] = t0[l]; sxy[l] = t1[l]; syy[l] = t2[l]; }
+    }
+    *sxx_o = sxx[0]; *sxy_o = sxy[0]; *syy_o = syy[0];
+}
+
 int or_ransac(const double *xy, int32_t n, double thr, int32_t T, uint32_t *key, int32_t *pos,
               const int32_t *hyp, uint8_t *mask, or_chunk_model *out, int32_t *draws_out,
               int32_t *cnt_out, double *sum_out) {
@@ -274,11 +302,8 @@ int or_ransac(const double *xy, int32_t n, double thr, int32_t T, uint32_t *key,
             else { sx += xy[2 * p]; sy += xy[2 * p + 1]; }
         }
         ox = sx / (double)nin; oy = sy / (double)nin;
-        double sxx = 0, sxy = 0, syy = 0;
-        for (int32_t p = 0; p < n; p++) if (mask[p]) {
-            double cx = xy[2 * p] - ox, cy = xy[2 * p + 1] - oy;
-            sxx += cx * cx; sxy += cx * cy; syy += cy * cy;
-        }
+        double sxx, sxy, syy;
+        scatter2(xy, mask, n, ox, oy, &sxx, &sxy, &syy);
         tls_direction(sxx, sxy, syy, &ux, &uy);
     }
     out->ox = ox; out->oy = oy; out->ux = ux; out->uy = uy;

@@ -289,3 +289,60 @@ def test_ukf_vs_oracle(ctx):
     # between two summation orders of the CPU oracle itself.
     assert np.max(np.abs(r["ukf_x"] - xo)) < 1e-4
     assert np.max(np.abs(r["ukf_P"] - Po)) < 1e-6
+
+
+def _border_batch():
+    """Chunks whose residuals sit on the inlier threshold (r^2 within ulps of
+    the cutoff, where the consensus kernel's cheap cross-product test defers to
+    the exact residual), duplicated points (degenerate hypotheses, u = d), and
+    mixtures of both."""
+    thr2 = [20.0, np.nextafter(20.0, 0), np.nextafter(20.0, 40), 19.999999999999996, 20.000000000000004]
+    chunks = []
+    xs = np.arange(0.0, 60.0, 1.5)
+    # 1) axis-aligned line + points at exactly/near the threshold distance
+    ys = np.zeros_like(xs)
+    ys[1::4] = [thr2[k % 5] * (1 if k % 2 else -1) for k in range(len(ys[1::4]))]
+    chunks.append(np.stack([xs, ys], 1))
+    # 2) the same rotated by 90 degrees, shifted
+    chunks.append(np.stack([ys + 1000.0, xs - 500.0], 1))
+    # 3) many duplicates: draws of two copies give a zero direction
+    d = np.array([[3.0, 4.0]] * 30 + [[3.0, 24.0]] * 10 + [[23.0, 4.0]] * 10 + [[100.0, 100.0]] * 5)
+    chunks.append(d)
+    # 4) duplicates on a line plus threshold-distance points
+    e = np.concatenate([np.stack([xs[:20], 2 * xs[:20]], 1), np.repeat([[7.0, 14.0]], 15, 0),
+                        np.stack([xs[:12], 2 * xs[:12] + 20.0 * np.sqrt(5.0)], 1)])
+    chunks.append(e)
+    # 5) every point on a slanted line: residuals ~1e-15, all 100 trials tied
+    chunks.append(np.stack([xs, 0.5 * xs + 3.0], 1))
+    # 6) every point on y = 7: residuals exactly 0, the zero-sum early stop
+    #    (the producer's draws for the following chunks are then replayed)
+    chunks.append(np.stack([xs, np.full_like(xs, 7.0)], 1))
+    chunks.append(chunks[0][::-1].copy())
+    return chunks
+
+
+def test_border_band_and_degenerate_hypotheses(ctx):
+    chunks = _border_batch()
+    seeds = np.arange(40, dtype=np.uint32) * 7919 + 11
+    S = len(seeds)
+    xy = np.concatenate([np.concatenate(chunks)] * S)
+    sizes = [len(c) for c in chunks] * S
+    cpo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    sco = (np.arange(S + 1) * len(chunks)).astype(np.int32)
+    g = {"xy": xy, "scan_chunk_off": sco, "chunk_pt_off": cpo}
+    r = _run_batch(ctx, g, seeds=seeds, assoc=False)
+    m = r["models"]
+    c = 0
+    for s in range(S):
+        st = orc.MTState(seed=int(seeds[s]))
+        for ch in chunks:
+            p0, p1 = cpo[c], cpo[c + 1]
+            mo, md, ex = orc.ransac(ch, 20.0, 100, state=st, want_trials=True)
+            assert np.array_equal(r["mask"][p0:p1], mo), (s, c)
+            assert np.array_equal(r["counts"][c], ex["cnt"]), (s, c)
+            for f in ("best_trial", "n_draws", "flags", "n_inliers"):
+                assert m[f][c] == md[f], (s, c, f)
+            for f in ("ox", "oy", "ux", "uy", "a", "b"):
+                assert m[f][c] == md[f] or (np.isnan(m[f][c]) and np.isnan(md[f])), (s, c, f)
+            c += 1
+        assert np.array_equal(r["mt_state"][s, :624], st.key) and r["mt_state"][s, 624] == st.pos.value, s
