@@ -30,8 +30,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec); the RANSAC residuals are FP64 VALU work
+VALU_PEAK_TOPS = 78.6     # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FLOPS_PER_EVAL = 12       # residual + inlier test per (point, hypothesis): SURVEY §8d
+OPS_PER_WORD = 20         # MT19937: twist 8 + temper 10 + masked compare 2 (per 32-bit word)
+OPS_PER_STEP = 5          # random_interval's mask for each Fisher-Yates step
+
+
+def mt_stream_ops(chunk_sizes, trials):
+    """Algorithmic 32-bit integer ops of the reference's sequential hypothesis
+    stream: per chunk of N >= 3 points, trials+1 draws of choice(N, 2) =
+    Fisher-Yates steps i = N-1..1, each consuming (m(i)+1)/(i+1) words on
+    average (random_interval's masked rejection, m(i) = 2^bitlen(i) - 1)."""
+    ops = 0.0
+    D = trials + 1
+    for n, cnt in zip(*np.unique(np.asarray(chunk_sizes), return_counts=True)):
+        if n < 3:
+            continue
+        i = np.arange(1, n, dtype=np.float64)
+        m = 2.0 ** np.floor(np.log2(i) + 1) - 1
+        words = np.sum((m + 1) / (i + 1))
+        ops += cnt * D * (OPS_PER_WORD * words + OPS_PER_STEP * (n - 1))
+    return ops
 
 
 def make_workload(scan_ids, n_beams, L, seed_base=0):
@@ -134,7 +154,7 @@ def main():
     ap.add_argument("--hyp", default="mt19937", choices=["mt19937", "philox"])
     ap.add_argument("--no-ukf", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=384)
+    ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-procs", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     ap.add_argument("--also-philox", action="store_true", help="also time the Philox (throughput) mode")
@@ -200,9 +220,13 @@ def main():
     ctx.timing_reset()
     elapsed = timed_region(step, args.steps, 0, sync_all, barrier)
     kms, klaunch = ctx.timing(_lib.K_PIPELINE)
+    rms, rl = ctx.timing(_lib.K_RNG)
+    cms, cl = ctx.timing(_lib.K_CONSENSUS)
     ctx.set_timing(False)
     elapsed = reduce_max(elapsed, dist)
     kavg = reduce_max(kms / max(klaunch, 1), dist)
+    ravg = reduce_max(rms / rl, dist) if rl else None
+    cavg = reduce_max(cms / max(cl, 1), dist)
 
     # sanity: results are well-formed (every chunk fitted or flagged)
     r = pipe.results()
@@ -210,21 +234,47 @@ def main():
 
     total_scans = S * world * args.steps
     value = total_scans / elapsed
-    evals = int(np.sum(np.diff(b["chunk_pt_off"])) * args.trials)   # (point, hypothesis) pairs per step
+    sizes = np.diff(b["chunk_pt_off"])
+    evals = int(np.sum(sizes) * args.trials)   # (point, hypothesis) pairs per step
     flops = FLOPS_PER_EVAL * evals
-    achieved_tf = flops / (kavg * 1e-3) / 1e12
+    cons_tf = flops / (cavg * 1e-3) / 1e12
     n_pts = int(b["chunk_pt_off"][-1])
     n_chunks = int(b["scan_chunk_off"][-1])
-    # algorithmic HBM bytes per launch: points in (16 B), mask (1 B) + projected y (8 B) out, chunk CSR
-    # (4 B) + model record (112 B) per chunk, per scan: seed, CSR, landmark count in/out + the list written
+    # algorithmic HBM bytes of the whole pipeline per step: points in (16 B), mask (1 B) + projected y
+    # (8 B) out, chunk CSR (4 B) + model record (112 B) per chunk, the draws handed from the producer to
+    # the consensus kernel (written + read), per scan: seed, CSR, landmark count in/out + the list written
     alg_bytes = n_pts * (16 + 1 + 8) + n_chunks * (4 + 112) + S * (4 + 4 + 8) + int(np.sum(r["lmk_count"])) * 56
+    if args.hyp == "mt19937":
+        alg_bytes += n_chunks * (args.trials + 1) * 8 * 2
     if not args.no_ukf:
         alg_bytes += S * (3 * 8 * 2 + 9 * 8 * 2 + 2 * 8 + 2 * L * 8 + 2 * L * 8)
     hbm_gbs = alg_bytes / (kavg * 1e-3) / 1e9
     traffic = load_traffic(args.traffic)
-    traffic_bytes = None
-    if traffic and traffic.get("scans") == S and traffic.get("hyp") == args.hyp:
-        traffic_bytes = traffic.get("bytes_per_launch")
+
+    def traffic_of(kernel):
+        if traffic and traffic.get("scans") == S and traffic.get("hyp") == args.hyp:
+            return (traffic.get("kernels") or {}).get(kernel, {}).get("bytes_per_launch")
+        return None
+
+    if args.hyp == "mt19937" and ravg:
+        # dominant kernel: the parity-stream producer (integer VALU, one serial chain per scan)
+        ops = mt_stream_ops(sizes, args.trials)
+        achieved = ops / (ravg * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": round(achieved, 4), "peak": VALU_PEAK_TOPS, "unit": "TOPS (int32)",
+                "frac": round(achieved / VALU_PEAK_TOPS, 5), "traffic": traffic_of("rng_kernel"),
+                "kernel": "rng_kernel (MT19937 parse, lslam_rng_pipe.h)", "kernel_ms": round(ravg, 4),
+                "ops_per_launch": round(ops), "ops_def": "%d per MT word (expected words from random_interval's "
+                "acceptance) + %d per Fisher-Yates step" % (OPS_PER_WORD, OPS_PER_STEP)}
+    else:
+        roof = {"bound": "fp64-valu", "achieved": round(cons_tf, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "traffic": traffic_of("chunk_kernel"),
+                "kernel": "chunk_kernel (consensus A4-A8)", "kernel_ms": round(cavg, 4), "flops_per_launch": flops}
+    roof.update({
+        "consensus": {"kernel": "chunk_kernel", "ms": round(cavg, 4), "fp64_tflops": round(cons_tf, 4),
+                      "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "flops_per_launch": flops},
+        "pipeline": {"ms": round(kavg, 4), "alg_bytes_per_launch": alg_bytes, "hbm_alg_gbs": round(hbm_gbs, 2),
+                     "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 5)},
+    })
 
     out = {
         "metric": "scans/sec (RANSAC+UKF, 720-pt scans) at 1/2/4/8 MI355X + HBM GB/s vs peak",
@@ -246,20 +296,7 @@ def main():
             "scans_per_gpu": S, "points_per_scan": args.beams, "trials": args.trials, "landmarks": L,
             "hyp": args.hyp, "parallelism": "dp%d (scan shards, no collective)" % world,
         },
-        "roofline": {
-            "bound": "fp64-valu",
-            "achieved": round(achieved_tf, 4),
-            "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5),
-            "traffic": traffic_bytes,
-            "kernel": "scan_kernel (lslam_scan_pipeline)",
-            "kernel_ms": round(kavg, 4),
-            "flops_per_launch": flops,
-            "alg_bytes_per_launch": alg_bytes,
-            "hbm_alg_gbs": round(hbm_gbs, 2),
-            "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 5),
-        },
+        "roofline": roof,
         "cpu_baseline": cpu,
         "valid_chunks": valid,
     }

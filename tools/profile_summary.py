@@ -23,22 +23,33 @@ def rows(path):
 
 
 def counter(path, name, kernel_sub="scan_kernel"):
-    vals = [float(r["Counter_Value"]) for r in rows(path)
-            if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == name]
-    return vals
+    """Per-dispatch sums (rows may be split per XCD/instance) of one counter."""
+    per = {}
+    for r in rows(path):
+        if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == name:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(per.values())
+
+
+# kernel-name substrings: producer, consensus, fix-up (scan_kernel<MT, RANSAC>), post pass (scan_kernel<EXPLICIT, ...>)
+KERNELS = {"rng_kernel": "rng_kernel", "chunk_kernel": "chunk_kernel", "fixup": "scan_kernel<0, 1>",
+           "post": "scan_kernel<2, "}
 
 
 def main(tag):
     os.makedirs(PROF, exist_ok=True)
     stats = rows(os.path.join(OUT, "prof_kt", "kt_kernel_stats.csv"))
     bench = [json.loads(l) for l in open(os.path.join(OUT, "bench.json")) if l.startswith("{")][-1]
-    fetch = counter(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = counter(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE")
-    f_kib = sum(fetch) / len(fetch) if fetch else None
-    w_kib = sum(write) / len(write) if write else None
-    traffic = None
-    if f_kib is not None and w_kib is not None:
-        traffic = int(2 * f_kib * 1024 + w_kib * 1024)
+    per = {}
+    for k, sub in KERNELS.items():
+        fetch = counter(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", sub)
+        write = counter(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE", sub)
+        if not fetch or not write:
+            continue
+        f_kib = sum(fetch) / len(fetch)
+        w_kib = sum(write) / len(write)
+        per[k] = {"fetch_kib": f_kib, "write_kib": w_kib, "bytes_per_launch": int(2 * f_kib * 1024 + w_kib * 1024),
+                  "avg_us": [float(r["AverageNs"]) / 1e3 for r in stats if sub in r["Name"]]}
     lines = ["# rocprofv3 summary: %s" % tag, "",
              "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2`",
              "(PMC: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes, --steps 3 --warmup 1)", "",
@@ -47,16 +58,16 @@ def main(tag):
         lines.append("| `%s` | %s | %.1f | %.1f | %.1f | %s |" % (
             r["Name"], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3,
             float(r["MaxNs"]) / 1e3, r["Percentage"]))
-    lines += ["", "PMC per scan_kernel launch: FETCH_SIZE %.1f KiB (x2 gfx950 correction), WRITE_SIZE %.1f KiB "
-              "-> traffic %s bytes/launch" % (f_kib or -1, w_kib or -1, traffic),
-              "", "bench.py line of the same build:", "", "```", json.dumps(bench), "```"]
+    lines += ["", "PMC HBM traffic per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE):", ""]
+    for k, v in per.items():
+        lines.append("- `%s`: FETCH_SIZE %.1f KiB, WRITE_SIZE %.1f KiB -> %d bytes/launch"
+                     % (k, v["fetch_kib"], v["write_kib"], v["bytes_per_launch"]))
+    lines += ["", "bench.py line of the same build:", "", "```", json.dumps(bench), "```"]
     open(os.path.join(PROF, "%s_rocprof.md" % tag), "w").write("\n".join(lines) + "\n")
     for src in ("prof_kt/kt_kernel_stats.csv",):
         data = open(os.path.join(OUT, src)).read()
         open(os.path.join(PROF, "%s_%s" % (tag, os.path.basename(src))), "w").write(data)
-    t = {"tag": tag, "scans": bench["config"]["scans_per_gpu"], "hyp": bench["config"]["hyp"],
-         "fetch_kib": f_kib, "write_kib": w_kib, "bytes_per_launch": traffic,
-         "kernel_avg_us": [float(r["AverageNs"]) / 1e3 for r in stats if "scan_kernel" in r["Name"]]}
+    t = {"tag": tag, "scans": bench["config"]["scans_per_gpu"], "hyp": bench["config"]["hyp"], "kernels": per}
     json.dump(t, open(os.path.join(PROF, "traffic_latest.json"), "w"), indent=1)
     json.dump(bench, open(os.path.join(PROF, "%s_bench.json" % tag), "w"))
     print("\n".join(lines))
