@@ -65,9 +65,11 @@ struct KArgs {
     int hist_cap;
     UkfConst ukf;
     // split pipeline
-    int32_t *hyp_scr;   // [n_chunks][T+1][2] draws from rng_kernel
-    uint32_t rjmask;    // rng_kernel: J ring size - 1
-    int off_blk, off_jr, off_fl, off_nxt, off_vtmp;
+    void *jbuf;         // producer -> consensus: Fisher-Yates j per step, [D * n_points] (u8 or u16)
+    int j8;             // jbuf holds u8
+    int res_g;          // resolve_kernel: LDS staging capacity (bytes)
+    int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
+    int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
@@ -751,13 +753,9 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
     const int lane = (int)threadIdx.x & 63;
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
-    RngPipe<JT> rp;
+    RngPipe rp;
     rp.blk = (uint32_t *)(smem + a.off_blk);
-    rp.jr = (JT *)(smem + a.off_jr);
-    rp.nxt = (uint32_t *)(smem + a.off_nxt);
     rp.fl = (lds_flag_t *)(smem + a.off_fl);
-    rp.rjmask = a.rjmask;
-    rp.nstride = (uint32_t)a.pts_cap;
 #ifdef LSLAM_STAMPS
     for (int k = 0; k < 8; k++) rp.acc[k] = 0;
     const uint64_t t_start = lslam_stamp();
@@ -778,8 +776,8 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
     __syncthreads();
     if (wave == 0) {
         // ---- parser: its chain is the kernel's critical path
-        rp.ndrawn = 0;
         rp.total_steps = 0;
+        rp.done_steps = 0;
         for (int c = c0; c < c1; c++) {
             const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
             if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
@@ -788,14 +786,16 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
         set_prio_level(2);
         int blkno = 0;
         int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
-        uint32_t gs = 0;
-        int dres_seen = 0;
+        JT *J = (JT *)a.jbuf;
         for (int c = c0; c < c1; c++) {
-            const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
+            const int p0 = B.chunk_pt_off[c];
+            const int N = B.chunk_pt_off[c + 1] - p0;
             if (N < 3) continue;
-            if (N >= 65) parse_chunk<true>(rp, blkno, pos, gs, dres_seen, (uint32_t)N, D, lane);
-            else parse_chunk<false>(rp, blkno, pos, gs, dres_seen, (uint32_t)N, D, lane);
+            JT *Jc = J + (size_t)D * (size_t)p0;
+            if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
         }
+        lds_flag_put(rp.fl + F_BLKUSE, -1);  // release the helper
         wake_helper();
         if (B.mt_state_out) {
             uint32_t *o = B.mt_state_out + (size_t)s * 625;
@@ -818,14 +818,32 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
         }
 #endif
     } else {
-        // ---- helper: short bursts (twist, resolve), asleep otherwise
+        // ---- helper: twists on demand, asleep otherwise
         __builtin_amdgcn_s_setprio(3);
 #ifdef LSLAM_STAMPS
         if (a.dbg && lane == 0)
             a.dbg[(size_t)s * 16 + 12] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
 #endif
-        rng_helper(rp, B, c0, c1, D, a.hyp_scr, lane);
+        rng_helper(rp, lane);
     }
+}
+
+// ------------------------------------------------------------------------
+// resolve_kernel: one wave per chunk, the producer's Fisher-Yates steps ->
+// the chunk's T+1 draws (lslam_rng_pipe.h: resolve_chunk)
+// ------------------------------------------------------------------------
+template <typename JT>
+__global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int c = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    if (N < 3) return;
+    const uint32_t D = (uint32_t)a.T + 1u;
+    resolve_chunk((const JT *)a.jbuf + (size_t)D * (size_t)p0, (uint32_t)N - 1u, D, (uint32_t)a.res_g, smem,
+                  a.draws_scr + (size_t)c * 2 * D, lane);
 }
 
 // ------------------------------------------------------------------------
@@ -880,7 +898,8 @@ __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
         if (B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
     } else {
-        const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.hyp_scr) + (size_t)c * 2 * D;
+        // explicit draws, or the parity stream's draws resolved by resolve_kernel
+        const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
         for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
@@ -1372,25 +1391,14 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     return LSLAM_OK;
 }
 
-// rng_kernel LDS: two raw MT blocks, the J ring (>= 2K + 128 steps, u8 when
-// every chunk has <= 256 points) + 64 dummy slots, RES_NB next-writer tables, flags
-static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, bool &j8) {
+// rng_kernel LDS: two raw MT blocks + flags
+static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
-    const int64_t steps = (int64_t)(b->max_scan_chunks > 0 ? b->max_scan_chunks : 1) * (k.T + 1) * (N - 1);
-    if (steps >= (1ll << 30)) return set_err(LSLAM_ERR_UNSUPPORTED, "too many Fisher-Yates steps per scan");
-    j8 = N <= 256;
-    int rj = 512;
-    while (rj < 2 * (N - 1) + 128) rj <<= 1;
-    k.rjmask = (uint32_t)rj - 1u;
-    k.pts_cap = N;  // next-writer table stride
     int off = 0;
     k.off_blk = off; off += align16(2 * 4 * 624);
-    k.off_jr = off; off += align16((j8 ? 1 : 2) * (rj + 64));
-    k.off_nxt = off; off += align16(4 * RES_NB * N);
     k.off_fl = off; off += align16(4 * F_NFLAGS);
     lds = off;
-    if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk size exceeds the 160 KiB LDS");
     return LSLAM_OK;
 }
 
@@ -1401,7 +1409,7 @@ static int ensure_scratch(lslam_ctx *c, size_t bytes) {
     c->scr = nullptr;
     c->scr_bytes = 0;
     hipError_t e = hipMalloc(&c->scr, bytes);
-    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (draw scratch)");
+    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (step scratch)");
     HIPCHK(e);
     c->scr_bytes = bytes;
     return LSLAM_OK;
@@ -1412,11 +1420,47 @@ static void set_max_lds(F *fn) {
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+// producer scratch: one j per Fisher-Yates step, D * n_points entries (chunk c at D * chunk_pt_off[c])
+// + the resolved draws [n_chunks][T+1][2] unless the caller asked for draws_out
+static int prepare_steps(lslam_ctx *c, KArgs &k) {
+    const int N = k.b.max_chunk_points;
+    k.j8 = N <= 256 ? 1 : 0;
+    const size_t jbytes = ((size_t)(k.T + 1) * (size_t)(k.b.n_points > 0 ? k.b.n_points : 1) * (k.j8 ? 1 : 2)
+                           + 64 + 255) & ~(size_t)255;  // 16-byte staging loads may run 15 bytes past the end
+    const size_t dbytes = k.b.draws_out ? 0 : (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4;
+    int st = ensure_scratch(c, jbytes + dbytes);
+    if (st) return st;
+    k.jbuf = c->scr;
+    k.draws_scr = k.b.draws_out ? k.b.draws_out : (int32_t *)((unsigned char *)c->scr + jbytes);
+    return LSLAM_OK;
+}
+
+// resolve_kernel LDS: the chunk's staged steps (if they fit)
+static int launch_resolve(lslam_ctx *c, const KArgs &base) {
+    if (base.b.n_chunks == 0) return LSLAM_OK;
+    KArgs k = base;
+    const int N = k.b.max_chunk_points > 3 ? k.b.max_chunk_points : 3;
+    const int esz = k.j8 ? 1 : 2;
+    // stage a chunk's steps in LDS when they fit 16 KiB (C3: 101 x 99 B), else stream them from HBM
+    const int64_t need = ((int64_t)(k.T + 1) * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
+    const int lds = need <= 16 * 1024 ? (int)need : 0;
+    k.res_g = lds;  // staging capacity in bytes
+    static std::once_flag once;
+    std::call_once(once, [] {
+        set_max_lds(resolve_kernel<uint8_t>);
+        set_max_lds(resolve_kernel<uint16_t>);
+    });
+    const dim3 grid((unsigned)k.b.n_chunks), block(64);
+    if (k.j8) hipLaunchKernelGGL(resolve_kernel<uint8_t>, grid, block, lds, c->stream, k);
+    else hipLaunchKernelGGL(resolve_kernel<uint16_t>, grid, block, lds, c->stream, k);
+    HIPCHK(hipGetLastError());
+    return LSLAM_OK;
+}
+
 static int launch_rng(lslam_ctx *c, const KArgs &base) {
     KArgs k = base;
     int lds = 0;
-    bool j8 = true;
-    int st = layout_rng(k, &k.b, lds, j8);
+    int st = layout_rng(k, &k.b, lds);
     if (st) return st;
     static std::once_flag once;
     std::call_once(once, [] {
@@ -1425,7 +1469,7 @@ static int launch_rng(lslam_ctx *c, const KArgs &base) {
     });
     st = timer_begin(c, LSLAM_K_RNG);
     if (st) return st;
-    if (j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
+    if (k.j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
     else hipLaunchKernelGGL(rng_kernel<uint16_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
     HIPCHK(hipGetLastError());
     return timer_end(c, LSLAM_K_RNG);
@@ -1477,13 +1521,8 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (st) return st;
     const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
     if (mt) {
-        if (b->draws_out) {
-            k.hyp_scr = b->draws_out;
-        } else {
-            st = ensure_scratch(c, (size_t)(b->n_chunks > 0 ? b->n_chunks : 1) * 2 * (k.T + 1) * sizeof(int32_t));
-            if (st) return st;
-            k.hyp_scr = (int32_t *)c->scr;
-        }
+        st = prepare_steps(c, k);
+        if (st) return st;
     }
     KArgs kp;
     int lds_post = 0;
@@ -1496,6 +1535,8 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (st) return st;
     if (mt) {
         st = launch_rng(c, k);
+        if (st) return st;
+        st = launch_resolve(c, k);
         if (st) return st;
     }
     st = launch_chunks(c, k, !assoc);
@@ -1550,10 +1591,14 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     if (st) return st;
     HIPCHK(hipSetDevice(c->device));
     if (b->n_scans == 0) return LSLAM_OK;
-    k.hyp_scr = b->draws_out;
+    k.hyp_source = LSLAM_HYP_MT19937;
+    st = prepare_steps(c, k);
+    if (st) return st;
     st = timer_begin(c, LSLAM_K_HYP);
     if (st) return st;
     st = launch_rng(c, k);
+    if (st) return st;
+    st = launch_resolve(c, k);
     if (st) return st;
     return timer_end(c, LSLAM_K_HYP);
 }

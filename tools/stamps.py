@@ -29,7 +29,7 @@ dbg.fill_zero()
 L.lslam_debug_set_stamps(dbg.ptr)
 pl.hyp_mt19937(ctx, b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.arange(S))
 acc = dbg.download().astype(np.float64)
-names = ["block_wait", "ring_wait", "fixed_point", "rest", "start_time", "windows", "fp_iterations",
+names = ["block_wait", "unused", "fixed_point", "rest", "start_time", "windows", "fp_iterations",
          "parser_total"]
 out = {n: round(float(np.mean(acc[:, k])), 1) for k, n in enumerate(names) if n not in ("start_time", "rest")}
 tot = acc[:, 7].mean()
