@@ -69,6 +69,7 @@ struct KArgs {
     int j8;             // jbuf holds u8
     int res_g;          // resolve_kernel: LDS staging capacity (bytes)
     int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
+    uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
@@ -553,7 +554,13 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         // early-stopped chunk consumed a different stream; replay it whole
         bool any = false;
         for (int c = c0 + lane; c < c1; c += 64) any |= (B.models[c].flags & LSLAM_EARLY_STOP) != 0;
-        if (ballot(any) == 0ull) return;
+        if (ballot(any) == 0ull) {
+            // the producer's end state is the scan's
+            if (B.mt_state_out && a.state_scr)
+                for (int i = lane; i < 625; i += 64)
+                    B.mt_state_out[(size_t)s * 625 + i] = a.state_scr[(size_t)s * 625 + i];
+            return;
+        }
     }
 
     MTWave mt;
@@ -944,9 +951,24 @@ struct lslam_ctx {
     int head[LSLAM_K_COUNT], npend[LSLAM_K_COUNT];
     double total_ms[LSLAM_K_COUNT];
     int64_t launches[LSLAM_K_COUNT];
-    // draws handed from rng_kernel to chunk_kernel when the caller gives no draws_out
+    // main-stream scratch: resolved draws (when the caller gives no draws_out)
     void *scr;
     size_t scr_bytes;
+    // The MT producer of call k+1 runs on its own stream while call k's
+    // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
+    // end-of-scan MT state), each released by an event once its consumers ran.
+    hipStream_t pstream;
+    void *pslot[2];
+    size_t pslot_bytes;
+    int next_slot;
+    hipEvent_t ev_slot_free[2];  // on stream, after the slot's resolve + fix-up
+    hipEvent_t ev_produced;      // on pstream, after rng_kernel
+    hipEvent_t ev_copy;          // on stream, after the latest lslam_h2d / lslam_memset
+    hipEvent_t ev_call;          // on stream, at the end of the latest pipeline call
+    // buffers written by the latest pipeline call (producer inputs must not alias them)
+    const void *out_ptr[12];
+    size_t out_len[12];
+    int n_out;
 };
 
 static thread_local std::string g_err;
@@ -1005,6 +1027,11 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->timing = false;
     c->scr = nullptr;
     c->scr_bytes = 0;
+    c->pstream = nullptr;
+    c->pslot[0] = c->pslot[1] = nullptr;
+    c->pslot_bytes = 0;
+    c->next_slot = 0;
+    c->n_out = 0;
     for (int k = 0; k < LSLAM_K_COUNT; k++) {
         c->total_ms[k] = 0;
         c->launches[k] = 0;
@@ -1022,6 +1049,16 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
             HIPCHK(hipEventCreate(&c->ev0[k][r]));
             HIPCHK(hipEventCreate(&c->ev1[k][r]));
         }
+    HIPCHK(hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[0], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[1], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_slot_free[0], c->stream));
+    HIPCHK(hipEventRecord(c->ev_slot_free[1], c->stream));
+    HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    HIPCHK(hipEventRecord(c->ev_call, c->stream));
     *out = c;
     return LSLAM_OK;
 }
@@ -1035,7 +1072,14 @@ int lslam_ctx_destroy(lslam_ctx *c) {
             if (c->ev0[k][r]) (void)hipEventDestroy(c->ev0[k][r]);
             if (c->ev1[k][r]) (void)hipEventDestroy(c->ev1[k][r]);
         }
+    if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->scr) (void)hipFree(c->scr);
+    for (int i = 0; i < 2; i++)
+        if (c->pslot[i]) (void)hipFree(c->pslot[i]);
+    hipEvent_t evs[5] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call};
+    for (hipEvent_t e : evs)
+        if (e) (void)hipEventDestroy(e);
+    if (c->pstream) (void)hipStreamDestroy(c->pstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -1044,6 +1088,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
 int lslam_sync(lslam_ctx *c) {
     if (!c) return LSLAM_ERR_ARG;
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->pstream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return LSLAM_OK;
 }
@@ -1083,6 +1128,7 @@ int lslam_h2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     return LSLAM_OK;
 }
 
@@ -1099,6 +1145,7 @@ int lslam_memset(lslam_ctx *c, void *dst, int v, size_t n) {
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(dst, v, n, c->stream));
+    HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     return LSLAM_OK;
 }
 
@@ -1116,17 +1163,17 @@ static int harvest(lslam_ctx *c, int k, int upto_free = -1) {
     return LSLAM_OK;
 }
 
-static int timer_begin(lslam_ctx *c, int k) {
+static int timer_begin(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
     if (!c->timing) return LSLAM_OK;
     int st = harvest(c, k, 1);
     if (st) return st;
-    HIPCHK(hipEventRecord(c->ev0[k][c->head[k]], c->stream));
+    HIPCHK(hipEventRecord(c->ev0[k][c->head[k]], st_ ? st_ : c->stream));
     return LSLAM_OK;
 }
 
-static int timer_end(lslam_ctx *c, int k) {
+static int timer_end(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
     if (!c->timing) return LSLAM_OK;
-    HIPCHK(hipEventRecord(c->ev1[k][c->head[k]], c->stream));
+    HIPCHK(hipEventRecord(c->ev1[k][c->head[k]], st_ ? st_ : c->stream));
     c->head[k] = (c->head[k] + 1) % LSLAM_EV_RING;
     c->npend[k] += 1;
     return LSLAM_OK;
@@ -1405,6 +1452,7 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
 static int ensure_scratch(lslam_ctx *c, size_t bytes) {
     if (c->scr_bytes >= bytes) return LSLAM_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->pstream));
     if (c->scr) HIPCHK(hipFree(c->scr));
     c->scr = nullptr;
     c->scr_bytes = 0;
@@ -1420,18 +1468,40 @@ static void set_max_lds(F *fn) {
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-// producer scratch: one j per Fisher-Yates step, D * n_points entries (chunk c at D * chunk_pt_off[c])
-// + the resolved draws [n_chunks][T+1][2] unless the caller asked for draws_out
-static int prepare_steps(lslam_ctx *c, KArgs &k) {
+// Producer slot: one j per Fisher-Yates step (D * n_points entries; chunk c at
+// D * chunk_pt_off[c]; + slack for 16-byte staging loads) and the end-of-scan
+// MT state.  The resolved draws live in the main-stream scratch unless the
+// caller asked for draws_out.
+static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     const int N = k.b.max_chunk_points;
     k.j8 = N <= 256 ? 1 : 0;
     const size_t jbytes = ((size_t)(k.T + 1) * (size_t)(k.b.n_points > 0 ? k.b.n_points : 1) * (k.j8 ? 1 : 2)
-                           + 64 + 255) & ~(size_t)255;  // 16-byte staging loads may run 15 bytes past the end
-    const size_t dbytes = k.b.draws_out ? 0 : (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4;
-    int st = ensure_scratch(c, jbytes + dbytes);
-    if (st) return st;
-    k.jbuf = c->scr;
-    k.draws_scr = k.b.draws_out ? k.b.draws_out : (int32_t *)((unsigned char *)c->scr + jbytes);
+                           + 64 + 255) & ~(size_t)255;
+    const size_t sbytes = (size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4;
+    if (c->pslot_bytes < jbytes + sbytes) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(c->pstream));
+        for (int i = 0; i < 2; i++) {
+            if (c->pslot[i]) HIPCHK(hipFree(c->pslot[i]));
+            c->pslot[i] = nullptr;
+        }
+        c->pslot_bytes = 0;
+        for (int i = 0; i < 2; i++) {
+            hipError_t e = hipMalloc(&c->pslot[i], jbytes + sbytes);
+            if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (producer slot)");
+            HIPCHK(e);
+        }
+        c->pslot_bytes = jbytes + sbytes;
+    }
+    k.jbuf = c->pslot[slot];
+    k.state_scr = (uint32_t *)((unsigned char *)c->pslot[slot] + jbytes);
+    if (k.b.draws_out) {
+        k.draws_scr = k.b.draws_out;
+    } else {
+        int st = ensure_scratch(c, (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4);
+        if (st) return st;
+        k.draws_scr = (int32_t *)c->scr;
+    }
     return LSLAM_OK;
 }
 
@@ -1457,7 +1527,7 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     return LSLAM_OK;
 }
 
-static int launch_rng(lslam_ctx *c, const KArgs &base) {
+static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
     int lds = 0;
     int st = layout_rng(k, &k.b, lds);
@@ -1467,12 +1537,45 @@ static int launch_rng(lslam_ctx *c, const KArgs &base) {
         set_max_lds(rng_kernel<uint8_t>);
         set_max_lds(rng_kernel<uint16_t>);
     });
-    st = timer_begin(c, LSLAM_K_RNG);
+    st = timer_begin(c, LSLAM_K_RNG, stream);
     if (st) return st;
-    if (k.j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
-    else hipLaunchKernelGGL(rng_kernel<uint16_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, c->stream, k);
+    if (k.j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, stream, k);
+    else hipLaunchKernelGGL(rng_kernel<uint16_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, stream, k);
     HIPCHK(hipGetLastError());
-    return timer_end(c, LSLAM_K_RNG);
+    return timer_end(c, LSLAM_K_RNG, stream);
+}
+
+static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+    if (!a || !b || !na || !nb) return false;
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x < y + nb && y < x + na;
+}
+
+// does the producer of this call read anything the previous pipeline call wrote?
+static bool producer_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
+    if (b->mt_state_in) return true;  // typically the previous call's mt_state_out
+    const void *in[3] = {b->seeds, b->scan_chunk_off, b->chunk_pt_off};
+    const size_t len[3] = {(size_t)b->n_scans * 4, (size_t)(b->n_scans + 1) * 4, (size_t)(b->n_chunks + 1) * 4};
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < c->n_out; j++)
+            if (ranges_overlap(in[i], len[i], c->out_ptr[j], c->out_len[j])) return true;
+    return false;
+}
+
+static void remember_outputs(lslam_ctx *c, const lslam_scan_batch *b, int T, int L) {
+    const size_t S = (size_t)b->n_scans, C = (size_t)b->n_chunks, P = (size_t)b->n_points;
+    const void *p[12] = {b->inlier_mask, b->models, b->y_proj, b->draws_out, b->trial_cnt_out, b->mt_state_out,
+                         b->landmarks, b->lmk_count, b->lmk_walk, b->ukf_x, b->ukf_P, nullptr};
+    const size_t n[12] = {P, C * sizeof(lslam_chunk_model), P * 8, C * 2 * (T + 1) * 4, C * T * 4, S * 625 * 4,
+                          S * b->lmk_capacity * sizeof(lslam_landmark), S * 4, S * b->lmk_capacity * 4,
+                          L ? S * 24 : 0, L ? S * 72 : 0, 0};
+    c->n_out = 0;
+    for (int i = 0; i < 12; i++)
+        if (p[i] && n[i]) {
+            c->out_ptr[c->n_out] = p[i];
+            c->out_len[c->n_out] = n[i];
+            c->n_out++;
+        }
 }
 
 static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
@@ -1520,9 +1623,11 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     int st = build_args(k, b, p, nullptr, MODE_RANSAC, lds_fix);
     if (st) return st;
     const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
+    const int slot = c->next_slot;
     if (mt) {
-        st = prepare_steps(c, k);
+        st = prepare_steps(c, k, slot);
         if (st) return st;
+        c->next_slot ^= 1;
     }
     KArgs kp;
     int lds_post = 0;
@@ -1534,8 +1639,17 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     st = timer_begin(c, LSLAM_K_PIPELINE);
     if (st) return st;
     if (mt) {
-        st = launch_rng(c, k);
+        // producer on its own stream: it waits for its slot's previous consumers, for input
+        // copies, and (on a hazard) for the previous call; the consumers wait for it
+        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
+        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
+        if (producer_hazard(c, b)) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
+        KArgs kr = k;
+        kr.b.mt_state_out = k.state_scr;
+        st = launch_rng(c, kr, c->pstream);
         if (st) return st;
+        HIPCHK(hipEventRecord(c->ev_produced, c->pstream));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
         st = launch_resolve(c, k);
         if (st) return st;
     }
@@ -1549,6 +1663,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3((unsigned)b->n_scans), dim3(64), lds_fix,
                            c->stream, kf);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     }
     switch (pmode) {
         case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post); break;
@@ -1557,6 +1672,8 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
+    remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
+    HIPCHK(hipEventRecord(c->ev_call, c->stream));
     return timer_end(c, LSLAM_K_PIPELINE);
 }
 
@@ -1592,14 +1709,18 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     HIPCHK(hipSetDevice(c->device));
     if (b->n_scans == 0) return LSLAM_OK;
     k.hyp_source = LSLAM_HYP_MT19937;
-    st = prepare_steps(c, k);
+    const int slot = c->next_slot;
+    st = prepare_steps(c, k, slot);
     if (st) return st;
+    c->next_slot ^= 1;
     st = timer_begin(c, LSLAM_K_HYP);
     if (st) return st;
-    st = launch_rng(c, k);
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_slot_free[slot], 0));
+    st = launch_rng(c, k, c->stream);  // on the main stream; the end state goes straight to mt_state_out
     if (st) return st;
     st = launch_resolve(c, k);
     if (st) return st;
+    HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     return timer_end(c, LSLAM_K_HYP);
 }
 
