@@ -32,7 +32,8 @@ def counter(path, name, kernel_sub="scan_kernel"):
 
 
 # kernel-name substrings: producer, consensus, fix-up (scan_kernel<MT, RANSAC>), post pass (scan_kernel<EXPLICIT, ...>)
-KERNELS = {"rng_kernel": "rng_kernel", "chunk_kernel": "chunk_kernel", "fixup": "scan_kernel<0, 1>",
+KERNELS = {"rng_kernel": "rng_kernel", "resolve_kernel": "resolve_kernel", "chunk_kernel": "chunk_kernel",
+           "fixup": "scan_kernel<0, 1>",
            "post": "scan_kernel<2, "}
 
 
