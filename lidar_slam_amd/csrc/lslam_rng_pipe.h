@@ -154,43 +154,54 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
         const uint32_t rem = G - g;
-        const uint32_t raw = (pre_pos == pos) ? pre_raw : kb[min(pos + lane, MT_N - 1)];
-        // next window's words (clamped inside the block; used only if the next window starts there)
-        pre_pos = pos + 64;
-        pre_raw = kb[min(pos + 64 + lane, MT_N - 1)];
-        const uint32_t w = mt_temper(raw);
-        RP_STAMP(3);
-        if (FAST && pos + 64 <= MT_N && rem > 64u) {
-            const uint32_t b1 = K - 1u - sg;
-            const uint32_t base0 = b1 - (uint32_t)lane;
-            uint32_t d = b1 - guess;
-            uint32_t i = fy_index(d, K);
-            uint32_t jv = fy_j(w, i);
-            uint64_t R = ballot(jv > i), Rp;
-            int it = 1;
-            do {
-                Rp = R;
-                d = mbcnt_from(Rp, base0);
-                i = fy_index(d, K);
-                jv = fy_j(w, i);
-                R = ballot(jv > i);
-                it++;
-            } while (R != Rp);
-            (void)it;
-            RP_STAMP(2);
-            RP_COUNT(5, 1);
-            RP_COUNT(6, it);
-            // R is the fixed point; d, i, jv belong to it.  The lane's reject
-            // bit is read back from R: a boolean carried out of the loop would
-            // be merged with exec on every iteration.
-            if (((uint32_t)(R >> lane) & 1u) == 0u) J[g + (b1 - d)] = (JT)jv;
-            const uint32_t na = 64u - (uint32_t)popc64(R);
-            pos += 64;
-            g += na;
-            sg += na;
-            if (sg >= K) sg -= K;
+        // a run of full windows: inside this block and short of the chunk's end
+        // (window r of the run still has > 64 steps left: r < (rem - 1) / 64)
+        const int nrun = FAST ? min((MT_N - pos) >> 6, (int)((rem - 1u) >> 6)) : 0;
+        if (nrun > 0) {
+            uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
+            for (int r = 0; r < nrun; r++) {
+                // next window's words (clamped inside the block; garbage past its end is never used)
+                const uint32_t nraw = kb[min(pos + 64 + lane, MT_N - 1)];
+                const uint32_t w = mt_temper(raw);
+                RP_STAMP(3);
+                const uint32_t b1 = K - 1u - sg;
+                const uint32_t base0 = b1 - (uint32_t)lane;
+                uint32_t d = b1 - guess;
+                uint32_t i = fy_index(d, K);
+                uint32_t jv = fy_j(w, i);
+                uint64_t R = ballot(jv > i), Rp;
+                int it = 1;
+                do {
+                    Rp = R;
+                    d = mbcnt_from(Rp, base0);
+                    i = fy_index(d, K);
+                    jv = fy_j(w, i);
+                    R = ballot(jv > i);
+                    it++;
+                } while (R != Rp);
+                (void)it;
+                RP_STAMP(2);
+                RP_COUNT(5, 1);
+                RP_COUNT(6, it);
+                // R is the fixed point; d, i, jv belong to it.  The lane's reject
+                // bit is read back from R: a boolean carried out of the loop would
+                // be merged with exec on every iteration.
+                if (((uint32_t)(R >> lane) & 1u) == 0u) J[g + (b1 - d)] = (JT)jv;
+                const uint32_t na = 64u - (uint32_t)popc64(R);
+                pos += 64;
+                g += na;
+                sg += na;
+                if (sg >= K) sg -= K;
+                raw = nraw;
+            }
+            pre_pos = pos;
+            pre_raw = raw;
             continue;
         }
+        const uint32_t raw = (pre_pos == pos) ? pre_raw : kb[min(pos + lane, MT_N - 1)];
+        pre_pos = -1;
+        const uint32_t w = mt_temper(raw);
+        RP_STAMP(3);
         // ---- partial window: block end, chunk end, or K < 64
         const int nw = min(64, MT_N - pos);
         const uint64_t actm = ballot(lane < nw);
