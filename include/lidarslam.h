@@ -12,6 +12,10 @@
  * fit.py = scikit-image 0.18.3 skimage/measure/fit.py, the third-party code the
  * reference calls):
  *   lslam_polar_to_xy     functions.py:59-60   (dX, dY of each measure)
+ *   lslam_express_decode  lidar.py:55-91 ExpressPacket.decode + :179-187
+ *                         _process_express_scan over the :327-338 measure stream
+ *   lslam_express_scans   the above + functions.py:56-76 (A1 + the A2 chunking of
+ *                         each revolution fed to rawPoints)
  *   lslam_hyp_mt19937     fit.py:819-826 random_state.choice(N, 2, replace=False)
  *                         on the global np.random legacy MT19937 stream
  *   lslam_ransac          ransac_functions.py:23-31  ransac(data, LineModelND, 2, 20,
@@ -161,6 +165,31 @@ typedef struct lslam_scan_batch {
     const double *ukf_R_diag;       /* [2L] measurement noise diagonal (systemClass.py:28) */
 } lslam_scan_batch;
 
+/* Express-scan measures (lslam_express_decode): device arrays, NULL = not written.
+ * Packet p (< M-1) yields measures 32p .. 32p+31 (trame 1..32, using packet p+1's start angle). */
+typedef struct lslam_express_measures {
+    double *angle_deg;    /* [(M-1)*32] lidar.py:185 (0 where invalid) */
+    double *dist_mm;      /* [(M-1)*32] ExpressPacket.distance (0 where invalid) */
+    uint8_t *new_scan;    /* [(M-1)*32] lidar.py:181-184 */
+    uint8_t *valid;       /* [(M-1)*32] packets p and p+1 both decode */
+    double *xy;           /* [(M-1)*32][2] functions.py:59-60 (A1 fused) */
+    uint8_t *pkt_valid;   /* [M] ExpressPacket.decode would not raise */
+} lslam_express_measures;
+
+/* Express-scan revolutions (lslam_express_scans): device arrays sized by the caller.
+ * Safe capacities for M packets: cap_points = 32(M-1), cap_scans = M-1,
+ * cap_chunks = 32(M-1)/100 + M-1.  counts (device, int32[4]) receives
+ * n_scans, n_chunks, n_points, and the packet holding the last new-revolution
+ * flag (-1 if none): resume the stream from that packet with skip = 1. */
+typedef struct lslam_express_revs {
+    double *xy;                 /* [cap_points][2] */
+    int32_t *scan_chunk_off;    /* [cap_scans + 1] CSR revolution -> chunks */
+    int32_t *chunk_pt_off;      /* [cap_chunks + 1] CSR chunk -> points */
+    int32_t *counts;            /* [4] */
+    int64_t cap_points;
+    int32_t cap_scans, cap_chunks;
+} lslam_express_revs;
+
 typedef struct lslam_ctx lslam_ctx;  /* opaque: device, stream, events, scratch */
 
 /* ---- library / context ---- */
@@ -180,7 +209,9 @@ int lslam_d2h(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* asy
 int lslam_memset(lslam_ctx *ctx, void *dst, int value, size_t bytes);     /* async */
 /* per-kernel HIP-event timing on the ctx stream (kernel ids: LSLAM_K_*) */
 enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMARK = 3, LSLAM_K_UKF = 4,
-       LSLAM_K_RNG = 5 /* parity-stream producer */, LSLAM_K_CONSENSUS = 6 /* per-chunk A4-A8 */, LSLAM_K_COUNT = 7 };
+       LSLAM_K_RNG = 5 /* parity-stream producer */, LSLAM_K_CONSENSUS = 6 /* per-chunk A4-A8 */,
+       LSLAM_K_EXPRESS = 7 /* a whole express decode / scans call */,
+       LSLAM_K_EXPRESS_SCATTER = 8 /* its decode + A1 + scatter kernel */, LSLAM_K_COUNT = 9 };
 int lslam_set_timing(lslam_ctx *ctx, int enable);
 int lslam_timing(lslam_ctx *ctx, int kernel, double *total_ms, int64_t *launches);  /* syncs */
 int lslam_timing_reset(lslam_ctx *ctx);
@@ -198,6 +229,13 @@ int lslam_mt_seed_state(uint32_t seed, uint32_t *state625);
 /* ---- hot path (device pointers, async on the ctx stream) ---- */
 /* A1: xy[i] = (d cos(-th*pi/180 + pi/2), d sin(...)); n measures */
 int lslam_polar_to_xy(lslam_ctx *ctx, const double *theta_deg, const double *dist, double *xy, int64_t n);
+/* E1: RPLidar express packets (M x 84 bytes, 4-byte aligned) -> measure stream */
+int lslam_express_decode(lslam_ctx *ctx, const uint8_t *packets, int64_t n_packets, const lslam_express_measures *out);
+/* E1 + A1 + A2: packets -> revolutions of chunked xy (functions.py:56-76); the first
+ * `skip` measures of packet 0 are dropped (a resumed stream).  Writes are clipped
+ * to the capacities; counts always holds the required sizes. */
+int lslam_express_scans(lslam_ctx *ctx, const uint8_t *packets, int64_t n_packets, int32_t skip,
+                        const lslam_express_revs *out);
 /* A3: the draws each chunk's ransac would make, assuming no early stop
  * (draws_out [n_chunks][max_trials+1][2]).  Uses b->seeds/mt_state_in/mt_state_out. */
 int lslam_hyp_mt19937(lslam_ctx *ctx, const lslam_scan_batch *b, int32_t max_trials);

@@ -27,6 +27,7 @@ CAPACITY = 256
 HYP_MT19937, HYP_PHILOX, HYP_EXPLICIT = 0, 1, 2
 UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC = 1, 2, 4
 K_POLAR, K_HYP, K_PIPELINE, K_LANDMARK, K_UKF, K_RNG, K_CONSENSUS = 0, 1, 2, 3, 4, 5, 6
+K_EXPRESS, K_EXPRESS_SCATTER = 7, 8
 
 
 class HIPLibraryError(RuntimeError):
@@ -70,6 +71,15 @@ class ScanBatch(C.Structure):
                                    "ukf_R_diag")]
 
 
+class ExpressMeasures(C.Structure):
+    _fields_ = [(n, _VP) for n in ("angle_deg", "dist_mm", "new_scan", "valid", "xy", "pkt_valid")]
+
+
+class ExpressRevs(C.Structure):
+    _fields_ = [(n, _VP) for n in ("xy", "scan_chunk_off", "chunk_pt_off", "counts")] + \
+               [("cap_points", C.c_int64), ("cap_scans", C.c_int32), ("cap_chunks", C.c_int32)]
+
+
 assert C.sizeof(ChunkModel) == 112
 assert C.sizeof(LandmarkRec) == 56
 
@@ -79,7 +89,7 @@ EXPORTS = [
     "lslam_h2d", "lslam_d2h", "lslam_memset", "lslam_set_timing", "lslam_timing", "lslam_timing_reset",
     "lslam_ransac_params_default", "lslam_ukf_params_default", "lslam_inlier_cutoff", "lslam_ukf_weights",
     "lslam_mt_seed_state", "lslam_polar_to_xy", "lslam_hyp_mt19937", "lslam_ransac", "lslam_landmarks",
-    "lslam_ukf_step", "lslam_scan_pipeline",
+    "lslam_ukf_step", "lslam_scan_pipeline", "lslam_express_decode", "lslam_express_scans",
 ]
 
 _lib = None
@@ -133,6 +143,8 @@ def load():
         "lslam_landmarks": ([_VP, P(ScanBatch), P(RansacParams)], C.c_int),
         "lslam_ukf_step": ([_VP, P(ScanBatch), P(UkfParams)], C.c_int),
         "lslam_scan_pipeline": ([_VP, P(ScanBatch), P(RansacParams), P(UkfParams)], C.c_int),
+        "lslam_express_decode": ([_VP, _VP, i64, P(ExpressMeasures)], C.c_int),
+        "lslam_express_scans": ([_VP, _VP, i64, i32, P(ExpressRevs)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -29,6 +29,7 @@
 #include <string>
 
 #include "../../include/lidarslam.h"
+#include "lslam_express.h"
 #include "lslam_rng.h"
 #include "lslam_rng_pipe.h"
 #include "lslam_ransac.h"
@@ -954,6 +955,9 @@ struct lslam_ctx {
     // main-stream scratch: resolved draws (when the caller gives no draws_out)
     void *scr;
     size_t scr_bytes;
+    // express-scan revolution builder scratch (per-packet flags/ranks, per-revolution info)
+    void *escr;
+    size_t escr_bytes;
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
@@ -1027,6 +1031,8 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->timing = false;
     c->scr = nullptr;
     c->scr_bytes = 0;
+    c->escr = nullptr;
+    c->escr_bytes = 0;
     c->pstream = nullptr;
     c->pslot[0] = c->pslot[1] = nullptr;
     c->pslot_bytes = 0;
@@ -1074,6 +1080,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
         }
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->scr) (void)hipFree(c->scr);
+    if (c->escr) (void)hipFree(c->escr);
     for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
     hipEvent_t evs[5] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call};
@@ -1677,6 +1684,32 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     return timer_end(c, LSLAM_K_PIPELINE);
 }
 
+
+// ---- express-scan codec (lslam_express.h) ----
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int ensure_escr(lslam_ctx *c, size_t bytes) {
+    if (c->escr_bytes >= bytes) return LSLAM_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->escr) HIPCHK(hipFree(c->escr));
+    c->escr = nullptr;
+    c->escr_bytes = 0;
+    hipError_t e = hipMalloc(&c->escr, bytes);
+    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (express scratch)");
+    HIPCHK(e);
+    c->escr_bytes = bytes;
+    return LSLAM_OK;
+}
+
+// packet streams are read as dwords: 4-byte alignment, and every rank fits int32
+static int express_check(const uint8_t *packets, int64_t n) {
+    if (n < 0 || (n > 0 && !packets)) return set_err(LSLAM_ERR_ARG, "express: bad packet stream");
+    if (((uintptr_t)packets & 3) != 0) return set_err(LSLAM_ERR_ARG, "express: packet stream must be 4-byte aligned");
+    if (n > ((int64_t)1 << 26)) return set_err(LSLAM_ERR_ARG, "express: more than 2^26 packets per call");
+    return LSLAM_OK;
+}
+
 extern "C" {
 
 int lslam_polar_to_xy(lslam_ctx *c, const double *th, const double *d, double *xy, int64_t n) {
@@ -1762,6 +1795,74 @@ int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ran
     int st = validate_batch(b, true);
     if (st) return st;
     return run_split(c, b, p, u);
+}
+
+int lslam_express_decode(lslam_ctx *c, const uint8_t *packets, int64_t n_packets, const lslam_express_measures *out) {
+    if (!c || !out) return LSLAM_ERR_ARG;
+    int st = express_check(packets, n_packets);
+    if (st) return st;
+    if (n_packets == 0) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    ExpressOut o{out->angle_deg, out->dist_mm, out->new_scan, out->valid, (double2 *)out->xy, out->pkt_valid};
+    if ((st = timer_begin(c, LSLAM_K_EXPRESS))) return st;
+    const int64_t blocks = (n_packets + EXP_DEC_PER_WG - 1) / EXP_DEC_PER_WG;
+    hipLaunchKernelGGL(express_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, packets, n_packets, o);
+    HIPCHK(hipGetLastError());
+    return timer_end(c, LSLAM_K_EXPRESS);
+}
+
+int lslam_express_scans(lslam_ctx *c, const uint8_t *packets, int64_t n_packets, int32_t skip,
+                        const lslam_express_revs *out) {
+    if (!c || !out || !out->counts || !out->scan_chunk_off || !out->chunk_pt_off) return LSLAM_ERR_ARG;
+    if (out->cap_scans < 0 || out->cap_chunks < 0 || out->cap_points < 0 || (out->cap_points > 0 && !out->xy))
+        return set_err(LSLAM_ERR_ARG, "express: bad output capacities");
+    int st = express_check(packets, n_packets);
+    if (st) return st;
+    if (skip < 0 || skip > 31) return set_err(LSLAM_ERR_ARG, "express: skip must be in [0, 31]");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t np = n_packets > 1 ? n_packets - 1 : 0;  // packets that carry measures
+    const int64_t tiles = (np + EXP_TILE - 1) / EXP_TILE;
+    size_t off = 0;
+    const size_t o_flags = off;
+    off = align256(off + (size_t)np);
+    const size_t o_tile = off;
+    off = align256(off + (size_t)tiles * sizeof(int2));
+    const size_t o_rank = off;
+    off = align256(off + (size_t)np * sizeof(int2));
+    const size_t o_rend = off;
+    off = align256(off + (size_t)np * sizeof(int2));
+    const size_t o_rinfo = off;
+    off = align256(off + (size_t)np * sizeof(int4));
+    if ((st = ensure_escr(c, off > 0 ? off : 256))) return st;
+    uint8_t *base = (uint8_t *)c->escr;
+    ExpressScratch s{base + o_flags, (int2 *)(base + o_tile), (int2 *)(base + o_rank), (int2 *)(base + o_rend),
+                     (int4 *)(base + o_rinfo), out->counts};
+    ExpressScans o{(double2 *)out->xy, out->scan_chunk_off, out->chunk_pt_off, out->cap_points, out->cap_scans,
+                   out->cap_chunks};
+    if ((st = timer_begin(c, LSLAM_K_EXPRESS))) return st;
+    if (tiles > 0) {
+        hipLaunchKernelGGL(express_flags_kernel, dim3((unsigned)tiles), dim3(256), 0, c->stream, packets, n_packets,
+                           (int)skip, s);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(express_rank_kernel, dim3((unsigned)tiles), dim3(256), 0, c->stream, n_packets, (int)skip, s);
+        HIPCHK(hipGetLastError());
+    }
+    // revolutions <= packets with measures: one 256-revolution workgroup per packet tile
+    hipLaunchKernelGGL(express_revs_kernel, dim3((unsigned)(tiles > 0 ? tiles : 1)), dim3(256), 0, c->stream,
+                       (int)tiles, s, o);
+    HIPCHK(hipGetLastError());
+    if (np > 0) {
+        if ((st = timer_begin(c, LSLAM_K_EXPRESS_SCATTER))) return st;
+        const int64_t blocks = (np + EXP_DEC_PER_WG - 1) / EXP_DEC_PER_WG;
+        hipLaunchKernelGGL(express_scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, packets, n_packets,
+                           (int)skip, s, o);
+        HIPCHK(hipGetLastError());
+        if ((st = timer_end(c, LSLAM_K_EXPRESS_SCATTER))) return st;
+    }
+    if ((st = timer_end(c, LSLAM_K_EXPRESS))) return st;
+    // the outputs may feed a pipeline call whose MT producer runs on the other stream
+    HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    return LSLAM_OK;
 }
 
 }  // extern "C"

@@ -40,7 +40,11 @@ class ScanPipeline:
                  landmarks=None, lmk_count=None, lmk_capacity=None, id_base=None,
                  ukf=None, want_draws=False, want_counts=False, want_yproj=True, want_state=False):
         self.ctx = ctx
-        xy = np.ascontiguousarray(xy, np.float64).reshape(-1, 2)
+        dev_xy = xy if isinstance(xy, DeviceArray) else None  # e.g. ExpressRevolutions.xy: stays on the device
+        if dev_xy is None:
+            xy = np.ascontiguousarray(xy, np.float64).reshape(-1, 2)
+        elif dev_xy.dtype != np.float64 or dev_xy.shape[-1] != 2:
+            raise ValueError("device xy must be float64 [n, 2]")
         sco = np.ascontiguousarray(scan_chunk_off, np.int32)
         cpo = np.ascontiguousarray(chunk_pt_off, np.int32)
         S = len(sco) - 1
@@ -58,7 +62,11 @@ class ScanPipeline:
         b.n_scans, b.n_chunks, b.n_points = S, Cn, P
         b.max_chunk_points = int(sizes.max()) if Cn else 0
         b.max_scan_chunks = int(per_scan.max()) if S else 0
-        b.xy = d(xy[:P] if P else np.zeros((1, 2)))
+        if dev_xy is not None:
+            self._keep.append(dev_xy)
+            b.xy = dev_xy.addr
+        else:
+            b.xy = d(xy[:P] if P else np.zeros((1, 2)))
         b.scan_chunk_off = d(sco)
         b.chunk_pt_off = d(cpo)
         self.hyp = HYP[hyp]

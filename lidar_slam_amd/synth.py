@@ -100,3 +100,42 @@ def make_batch(scan_ids, n_beams: int = 720, cfg: int = 0):
         "chunk_pt_off": np.asarray(cpo, dtype=np.int32),
         "poses": np.asarray(poses),
     }
+
+
+def express_packets(n_packets: int, per_rev: float = 22.5, seed: int = 0, corrupt: float = 0.0,
+                    scan_id: int | None = None):
+    """A synthetic RPLidar express stream (lidar.py:59-91 layout), uint8 [M, 84].
+
+    Start angles advance 360/per_rev degrees per packet (jittered) and wrap once
+    per revolution, so a revolution holds ~32*per_rev measures (720 at the
+    default 22.5).  Cabin bytes are random unless ``scan_id`` is given, in which
+    case the 10-bit-shifted distances follow ``scan_polar(scan_id)``'s ranges.
+    A fraction ``corrupt`` of the packets gets a broken checksum or sync nibble.
+    """
+    rng = np.random.default_rng(7_000_003 * seed + 11)
+    M = int(n_packets)
+    pk = rng.integers(0, 256, (M, 84), dtype=np.uint8)
+    step = 360.0 / per_rev
+    jit = 0.1 * min(step, 360.0 - step)
+    ang = (rng.uniform(0, step) + step * np.arange(M) + rng.uniform(-jit, jit, M)) % 360.0
+    q6 = (np.floor(ang * 64).astype(np.int64)) % (360 * 64)
+    pk[:, 2] = q6 & 0xFF
+    pk[:, 3] = ((q6 >> 8) & 0x7F) | np.where(rng.random(M) < 0.02, 0x80, 0)
+    if scan_id is not None:
+        _, d, _ = scan_polar(scan_id, n_beams=max(M * 32, 1))
+        dq = np.clip(np.round(d[:M * 32]), 0, (1 << 14) - 1).astype(np.int64).reshape(M, 16, 2)
+        i = 5 * np.arange(16)
+        for h, (lo, hi) in enumerate(((4, 5), (6, 7))):
+            keep = pk[:, i + lo] & 3  # the angle-offset bits share the low byte
+            pk[:, i + lo] = ((dq[:, :, h] & 0x3F) << 2).astype(np.uint8) | keep
+            pk[:, i + hi] = (dq[:, :, h] >> 6).astype(np.uint8)
+    cs = np.bitwise_xor.reduce(pk[:, 2:], axis=1)
+    pk[:, 0] = 0xA0 | (cs & 0x0F)
+    pk[:, 1] = 0x50 | (cs >> 4)
+    if corrupt > 0:
+        bad = np.nonzero(rng.random(M) < corrupt)[0]
+        kind = rng.integers(0, 3, bad.size)
+        pk[bad[kind == 0], 0] ^= 0x40          # sync nibble
+        pk[bad[kind == 1], 1] ^= 0x01          # checksum nibble
+        pk[bad[kind == 2], 40] ^= 0x08         # payload byte
+    return pk

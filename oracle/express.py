@@ -68,3 +68,55 @@ def measures(dec):
     ok2 = np.repeat(ok[:, None], 32, 1)
     return dict(m_ok=ok2.astype(np.uint8), m_new=(new & ok2).astype(np.uint8), m_ang=np.where(ok2, ang, 0.0),
                 m_dist=np.where(ok2, dec["dist"][:-1], 0))
+
+
+def capture(packets, drop=0, chunk=100, min_rem=2):
+    """functions.py:47-81 over the measure stream of `packets` (the capture
+    loop; the first `drop` measures are the 1-second warm-up of :58).
+
+    Restated as the reference's per-measure state machine: append (dX, dY)
+    (:59-63); every `chunk` points put the list (:64-67); on the
+    new-revolution flag put the remainder if it has more than `min_rem` points,
+    then the delimiter 0 (:68-76).  Measures of packets that fail to decode
+    are skipped (the reference raises instead).  Returns dict(xy [P, 2],
+    chunk_sizes, delim) in the format of tests/golden/express.npz's cap* keys:
+    delim[r] = number of chunks put before revolution r's 0.
+    """
+    m = measures(decode_packets(packets))
+    ok, new, ang, dist = (m[k].ravel() for k in ("m_ok", "m_new", "m_ang", "m_dist"))
+    pts, xy, sizes, delim = [], [], [], []
+    for i in range(drop, ok.size):
+        if not ok[i]:
+            continue
+        d, a = float(dist[i]), float(ang[i])
+        pts.append((d * np.cos(-a * (np.pi / 180) + np.pi / 2), d * np.sin(-a * (np.pi / 180) + np.pi / 2)))
+        if len(pts) == chunk:
+            xy += pts
+            sizes.append(len(pts))
+            pts = []
+        if new[i]:
+            if len(pts) > min_rem:
+                xy += pts
+                sizes.append(len(pts))
+            delim.append(len(sizes))
+            pts = []
+    return dict(xy=np.array(xy, np.float64).reshape(-1, 2), chunk_sizes=np.array(sizes, np.int32),
+                delim=np.array(delim, np.int32))
+
+
+def revolutions(packets, skip=0):
+    """The completed revolutions of `packets` as CSR (what lslam_express_scans
+    returns): xy [P, 2], scan_chunk_off [S+1], chunk_pt_off [C+1], and the
+    packet holding the last new-revolution flag (-1 if none).  Chunks of the
+    open revolution after the last flag are not included."""
+    cap = capture(packets, drop=skip)
+    S = len(cap["delim"])
+    C = int(cap["delim"][-1]) if S else 0
+    sizes = cap["chunk_sizes"][:C]
+    cpo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    sco = np.concatenate([[0], cap["delim"]]).astype(np.int32)
+    m = measures(decode_packets(packets))["m_new"]
+    flagged = np.nonzero(m[:, 0])[0]
+    flagged = flagged[flagged > 0] if skip else flagged
+    resume = int(flagged[-1]) if flagged.size else -1
+    return dict(xy=cap["xy"][:cpo[-1]], scan_chunk_off=sco, chunk_pt_off=cpo, resume=resume)

@@ -15,6 +15,12 @@ module.  Recorded, for a synthetic stream of 84-byte express packets:
     179-187): for each packet p with a successor, 32 (new_scan, angle,
     distance) computed by ``Lidar._process_express_scan`` from p and the next
     packet's start_angle.
+  * the capture loop ``functions.scanning(rawPoints)`` (functions.py:47-81,
+    unmodified; ``mainWindow`` stubbed as in make_golden.py) run over a
+    stand-in ``Lidar`` whose ``scan('express')`` yields exactly the measure
+    stream above, with ``time.time`` faked so that the first ``drop``
+    measures fall inside the 1-second warm-up: every ``rawPoints.put`` (a
+    chunk of [dX, dY] or the revolution delimiter 0) is recorded.
 Output: tests/golden/express.npz (plain arrays, no pickles).
 """
 import os
@@ -29,6 +35,12 @@ sys.path.insert(0, REF)
 sys.modules["serial"] = types.ModuleType("serial")  # only the port methods use it
 
 import lidar  # noqa: E402  (reference, unmodified)
+
+_stub = types.ModuleType("mainWindow")  # mainWindow.py needs the absent PyQt5.QtChart
+_stub.time = __import__("time")
+_stub.ploting = lambda *a, **k: None
+sys.modules["mainWindow"] = _stub
+import functions  # noqa: E402  (reference, unmodified)
 
 
 def make_packets(n_rev=3, per_rev=24, seed=7):
@@ -51,6 +63,80 @@ def make_packets(n_rev=3, per_rev=24, seed=7):
         ang = (ang + 360.0 / per_rev + rng.uniform(-0.3, 0.3)) % 360.0
     # edge angles: exactly 0 and the largest start angle, and a wrap to 0
     return pk
+
+
+def make_revolutions(rev_packets, seed):
+    """Clean packets whose start angles wrap after exactly rev_packets[r]
+    packets per revolution (the first and last revolutions are open)."""
+    rng = np.random.default_rng(seed)
+    pk = []
+    for k in rev_packets:
+        for i in range(k):
+            b = bytearray(rng.integers(0, 256, 84, dtype=np.uint8).tobytes())
+            q6 = int((i + rng.uniform(0.05, 0.6)) * 360 * 64 / k) % (360 * 64)
+            b[2] = q6 & 0xFF
+            b[3] = ((q6 >> 8) & 0x7F) | (0x80 if rng.random() < 0.05 else 0)
+            cs = 0
+            for x in b[2:]:
+                cs ^= x
+            b[0] = 0xA0 | (cs & 0x0F)
+            b[1] = 0x50 | (cs >> 4)
+            pk.append(bytes(b))
+    return pk
+
+
+class _Queue:
+    def __init__(self):
+        self.items = []
+
+    def put(self, x):
+        self.items.append(x)
+
+
+def capture(stream, drop):
+    """functions.scanning over a stand-in Lidar yielding the reference's
+    measure stream of `stream`; the first `drop` measures are warm-up."""
+    dec = [lidar.ExpressPacket.decode(raw) for raw in stream]
+    L = object.__new__(lidar.Lidar)
+
+    class FakeLidar:
+        def __init__(self, port):
+            pass
+
+        def scan(self, scan_type, max_buf_meas=False, speed=0):
+            for p in range(len(dec) - 1):
+                for t in range(1, 33):
+                    yield L._process_express_scan(dec[p], dec[p + 1].start_angle, t), 0.0
+
+    clock = {"n": -1}
+
+    def fake_time():  # call 0 = start_time; call i >= 1 = measure i-1
+        clock["n"] += 1
+        return 0.0 if clock["n"] <= drop else 2.0
+
+    q = _Queue()
+    saved = functions.Lidar, functions.time
+    functions.Lidar = FakeLidar
+    functions.time = types.SimpleNamespace(time=fake_time)
+    try:
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO()):
+            functions.scanning(q)
+    finally:
+        functions.Lidar, functions.time = saved
+    # flatten: xy of every chunk, chunk sizes, and after how many chunks each 0 came
+    xy, sizes, delim = [], [], []
+    for it in q.items:
+        if isinstance(it, int) and it == 0:
+            delim.append(len(sizes))
+        else:
+            a = np.asarray(it, np.float64).reshape(-1, 2)
+            xy.append(a)
+            sizes.append(len(a))
+    xy = np.concatenate(xy) if xy else np.zeros((0, 2))
+    return dict(packets=np.frombuffer(b"".join(stream), np.uint8).reshape(len(stream), 84),
+                drop=np.int32(drop), xy=xy, chunk_sizes=np.array(sizes, np.int32), delim=np.array(delim, np.int32))
 
 
 def corrupt(pk, rng):
@@ -119,6 +205,14 @@ def main():
         for k, v in r.items():
             flat["%s_%s" % (name, k)] = v
     flat["bad_index"] = np.array(sorted(bad), np.int32)
+    # capture loop: (A) first revolution of 289 - 88 = 201 points (remainder 1
+    # dropped), a 1-packet revolution, an 800-point one; (B) 161 - 59 = 102
+    # (remainder 2 dropped), a 2-packet revolution, a 3-packet one
+    caps = {"capA": capture(make_revolutions([10, 23, 1, 25, 22, 7], 5), 88),
+            "capB": capture(make_revolutions([6, 2, 3, 24, 21, 4], 6), 59)}
+    for name, r in caps.items():
+        for k, v in r.items():
+            flat["%s_%s" % (name, k)] = v
     np.savez_compressed(os.path.join(HERE, "express.npz"), **flat)
     print("express.npz:", {k: v.shape for k, v in flat.items()})
 
