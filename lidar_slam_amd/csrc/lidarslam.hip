@@ -74,6 +74,9 @@ struct KArgs {
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
+    // large chunks (N > 128): count_kernel -> select_kernel
+    int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
+    int cnt_blocks;     // count_kernel workgroups per chunk
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
 };
 
@@ -925,6 +928,324 @@ __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
     if (lane == 0 && B.models) B.models[c] = rec;
 }
 
+// ------------------------------------------------------------------------
+// Large chunks (N > 128, e.g. C5: 4096 points x 2048 hypotheses).  The
+// count pass is split from the selection so that it can use many waves per
+// chunk with the points in LDS shared by all of them:
+//   count_kernel   workgroup = 256 lanes x CNT_HPT hypotheses of one chunk;
+//                  lanes keep their hypotheses in registers and stream the
+//                  chunk's points as LDS broadcasts (the cheap cross-product
+//                  test of chunk_consensus, two cutoffs instead of a band test;
+//                  a hypothesis with a point inside the band, a non-unit
+//                  direction or non-finite data is recounted exactly).
+//   select_kernel  one wave per chunk: max count, tied trials, tie brackets,
+//                  exact pairwise sums of the candidates (lanes over points),
+//                  then the same finish as chunk_kernel.
+// ------------------------------------------------------------------------
+constexpr int CNT_TPB = 256;
+constexpr int CNT_HPT = 4;
+constexpr int CNT_TRIALS_PER_WG = CNT_TPB * CNT_HPT;
+
+// bounding-box E2 and finiteness of P[0..N) (every lane gets the same values)
+struct ChunkBox {
+    double E2;
+    bool finite;
+};
+
+__device__ __forceinline__ void box_partial(const double2 *src, int N, int tid, int nthr, double2 *P, double &xmn,
+                                            double &xmx, double &ymn, double &ymx, bool &fin) {
+    xmn = __builtin_inf(); xmx = -__builtin_inf(); ymn = __builtin_inf(); ymx = -__builtin_inf();
+    fin = true;
+    for (int p = tid; p < N; p += nthr) {
+        const double2 q = src[p];
+        if (P) P[p] = q;
+        xmn = fmin(xmn, q.x); xmx = fmax(xmx, q.x);
+        ymn = fmin(ymn, q.y); ymx = fmax(ymx, q.y);
+        fin = fin && (q.x - q.x == 0.0) && (q.y - q.y == 0.0);
+    }
+    xmn = wave_min_d(xmn); xmx = wave_max_d(xmx);
+    ymn = wave_min_d(ymn); ymx = wave_max_d(ymx);
+}
+
+__device__ __forceinline__ ChunkBox box_finish(double xmn, double xmx, double ymn, double ymx, bool fin) {
+    const double bx = xmx - xmn, by = ymx - ymn;
+    ChunkBox b;
+    b.E2 = (bx * bx + by * by) * (1.0 + 0x1p-20);
+    b.finite = fin && b.E2 < __builtin_inf();
+    return b;
+}
+
+// the hypothesis pair of trial t (draw t) of chunk c
+template <int HYP>
+__device__ __forceinline__ void trial_pair(const KArgs &a, int c, int N, int D, int t, int32_t &i0, int32_t &i1) {
+    if (HYP == LSLAM_HYP_PHILOX) {
+        philox_pair((uint32_t)N, (uint32_t)t, (uint32_t)c, a.philox_seed, i0, i1);
+    } else {
+        const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? a.b.hyp : a.draws_scr) + ((size_t)c * D + t) * 2;
+        i0 = h[0];
+        i1 = h[1];
+    }
+}
+
+// exact count of one hypothesis: the cheap test where it is decisive
+__device__ __forceinline__ int exact_count(const double2 *P, int N, const Model &m, bool exact_all, double ecut,
+                                           double margin) {
+    int c = 0;
+    for (int p = 0; p < N; p++) {
+        const double2 q = P[p];
+        const double ex = q.x - m.ox, ey = q.y - m.oy;
+        const double r = __builtin_fma(ex, m.uy, -(ey * m.ux));
+        const double v = r * r;
+        bool in = v < ecut;
+        if (exact_all || fabs(v - ecut) <= margin) in = resid2(q, m) < ecut;
+        c += (int)in;
+    }
+    return c;
+}
+
+template <int HYP>
+__global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
+    // dynamic LDS only (a static part would push the 160 KiB request over the limit):
+    // the chunk's points, then the per-wave box / finiteness partials
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const lslam_scan_batch &B = a.b;
+    const int c = (int)blockIdx.x / a.cnt_blocks, tb = (int)blockIdx.x % a.cnt_blocks;
+    const int tid = (int)threadIdx.x, w = tid >> 6;
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    double2 *P = (double2 *)smem;
+    double(*s_box)[4] = (double(*)[4])(smem + ((16 * N + 15) & ~15));
+    int *s_fin = (int *)(s_box + 4);
+    if (N < 3) return;
+    const int T = a.T, D = T + 1;
+    double xmn, xmx, ymn, ymx;
+    bool fin;
+    box_partial((const double2 *)B.xy + p0, N, tid, CNT_TPB, P, xmn, xmx, ymn, ymx, fin);
+    const bool wfin = ballot(!fin) == 0ull;
+    if ((tid & 63) == 0) {
+        s_box[w][0] = xmn; s_box[w][1] = xmx; s_box[w][2] = ymn; s_box[w][3] = ymx;
+        s_fin[w] = wfin;
+    }
+    __syncthreads();
+    xmn = fmin(fmin(s_box[0][0], s_box[1][0]), fmin(s_box[2][0], s_box[3][0]));
+    xmx = fmax(fmax(s_box[0][1], s_box[1][1]), fmax(s_box[2][1], s_box[3][1]));
+    ymn = fmin(fmin(s_box[0][2], s_box[1][2]), fmin(s_box[2][2], s_box[3][2]));
+    ymx = fmax(fmax(s_box[0][3], s_box[1][3]), fmax(s_box[2][3], s_box[3][3]));
+    const ChunkBox bx = box_finish(xmn, xmx, ymn, ymx, s_fin[0] && s_fin[1] && s_fin[2] && s_fin[3]);
+    const double ecut = a.ecut;
+    const bool cheap = bx.finite && ecut < __builtin_inf();
+    const double margin = (bx.E2 + ecut) * 0x1p-42;
+    const double elo = ecut - margin, ehi = ecut + margin;
+    Model m[CNT_HPT];
+    bool ex[CNT_HPT];
+    int lo[CNT_HPT], hi[CNT_HPT];
+#pragma unroll
+    for (int h = 0; h < CNT_HPT; h++) {
+        const int t = tb * CNT_TRIALS_PER_WG + h * CNT_TPB + tid;
+        int32_t i0 = 0, i1 = 1;
+        if (t < T) {
+            trial_pair<HYP>(a, c, N, D, t, i0, i1);
+            if (HYP == LSLAM_HYP_PHILOX) {  // the draws select_kernel (and draws_out) read
+                int32_t *o = a.draws_scr + ((size_t)c * D + t) * 2;
+                o[0] = i0;
+                o[1] = i1;
+            }
+        }
+        m[h] = model2(P[i0], P[i1]);
+        const double un = m[h].ux * m[h].ux + m[h].uy * m[h].uy;
+        ex[h] = !cheap || !(fabs(un - 1.0) <= 0x1p-46);
+        lo[h] = 0;
+        hi[h] = 0;
+    }
+    if (HYP == LSLAM_HYP_PHILOX && tb == a.cnt_blocks - 1 && tid == 0) {  // draw T: drawn, never a trial
+        int32_t i0, i1;
+        philox_pair((uint32_t)N, (uint32_t)T, (uint32_t)c, a.philox_seed, i0, i1);
+        a.draws_scr[((size_t)c * D + T) * 2] = i0;
+        a.draws_scr[((size_t)c * D + T) * 2 + 1] = i1;
+    }
+    int p = 0;
+    for (; p + 2 <= N; p += 2) {
+        const double2 q0 = P[p], q1 = P[p + 1];
+#pragma unroll
+        for (int h = 0; h < CNT_HPT; h++) {
+            const double e0x = q0.x - m[h].ox, e0y = q0.y - m[h].oy;
+            const double e1x = q1.x - m[h].ox, e1y = q1.y - m[h].oy;
+            const double r0 = __builtin_fma(e0x, m[h].uy, -(e0y * m[h].ux));
+            const double r1 = __builtin_fma(e1x, m[h].uy, -(e1y * m[h].ux));
+            const double v0 = r0 * r0, v1 = r1 * r1;
+            lo[h] += (int)(v0 < elo) + (int)(v1 < elo);
+            hi[h] += (int)(v0 <= ehi) + (int)(v1 <= ehi);
+        }
+    }
+    for (; p < N; p++) {
+        const double2 q = P[p];
+#pragma unroll
+        for (int h = 0; h < CNT_HPT; h++) {
+            const double exx = q.x - m[h].ox, eyy = q.y - m[h].oy;
+            const double r = __builtin_fma(exx, m[h].uy, -(eyy * m[h].ux));
+            const double v = r * r;
+            lo[h] += (int)(v < elo);
+            hi[h] += (int)(v <= ehi);
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < CNT_HPT; h++) {
+        const int t = tb * CNT_TRIALS_PER_WG + h * CNT_TPB + tid;
+        if (t >= T) continue;
+        int cnt = lo[h];
+        if (ex[h] || lo[h] != hi[h]) cnt = exact_count(P, N, m[h], ex[h], ecut, margin);  // rare
+        a.cnt_scr[(size_t)c * T + t] = cnt;
+    }
+}
+
+template <int HYP>
+__global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int c = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    double2 *P = (double2 *)(smem + a.off_pts);
+    int32_t *tied = (int32_t *)(smem + a.off_tied);
+    double *tsum = (double *)(smem + a.off_tsum);
+    int32_t *inl = (int32_t *)(smem + a.off_inl);
+    uint8_t *mk = (uint8_t *)(smem + a.off_mask);
+    double *vst = (double *)(smem + a.off_vstack);
+    int *nstack = (int *)(smem + a.off_nstack);
+    double *vtmp = (double *)(smem + a.off_vtmp);
+    int lo = 0, hi = B.n_scans;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (B.scan_chunk_off[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    const int s = uni(lo);
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    const int T = a.T, D = T + 1;
+    lslam_chunk_model rec;
+    memset(&rec, 0, sizeof(rec));
+    rec.best_trial = -1;
+    rec.match_index = -1;
+    rec.landmark_id = (B.id_base ? B.id_base[s] : 0) + (c - B.scan_chunk_off[s]);
+    rec.n_points = N;
+    if (N < 3) {
+        rec.flags = LSLAM_N_TOO_SMALL;
+        if (lane == 0 && B.models) B.models[c] = rec;
+        for (int p = lane; p < N; p += 64) {
+            if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
+            if (B.y_proj && a.write_yproj) B.y_proj[p0 + p] = 0.0;
+        }
+        return;
+    }
+    const int32_t *draws = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
+    if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
+        for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
+    double xmn, xmx, ymn, ymx;
+    bool fin;
+    box_partial((const double2 *)B.xy + p0, N, lane, 64, P, xmn, xmx, ymn, ymx, fin);
+    const ChunkBox bx = box_finish(unid(xmn), unid(xmx), unid(ymn), unid(ymx), ballot(!fin) == 0ull);
+    __syncthreads();
+    const double ecut = a.ecut;
+    const bool cheap = bx.finite && ecut < __builtin_inf();
+    const int32_t *cnt = a.cnt_scr + (size_t)c * T;
+    int M = 0;
+    for (int t = lane; t < T; t += 64) M = max(M, cnt[t]);
+    M = uni(wave_max(M));
+    int ntied = 0;
+    for (int tb = 0; tb < T; tb += 64) {
+        const int t = tb + lane;
+        const bool h = t < T && cnt[t] == M;
+        const uint64_t bm = ballot(h);
+        if (h) tied[ntied + (int)mbcnt(bm)] = t;
+        ntied += popc64(bm);
+    }
+    __syncthreads();
+    ChunkOut o;
+    o.flags = 0;
+    o.best = -1;
+    o.stop = -1;
+    o.n_inl = 0;
+    o.last_inl = -1;
+    o.n_draws = D;
+    int best = -1;
+    if (T > 0) {
+        const bool need_sums = ntied > 1 || M == N || !(ecut > 0.0);
+        if (!need_sums) {
+            best = tied[0];
+        } else {
+            // brackets of the tied trials' sums (-1: always a candidate)
+            for (int k = lane; k < ntied; k += 64) {
+                const int t = tied[k];
+                const Model m = model2(P[draws[2 * t]], P[draws[2 * t + 1]]);
+                const double un = m.ux * m.ux + m.uy * m.uy;
+                double S = -1.0;
+                if (cheap && fabs(un - 1.0) <= 0x1p-46) {
+                    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+                    int p = 0;
+                    for (; p + 4 <= N; p += 4) {
+                        const double2 q0 = P[p], q1 = P[p + 1], q2 = P[p + 2], q3 = P[p + 3];
+                        const double r0 = __builtin_fma(q0.x - m.ox, m.uy, -((q0.y - m.oy) * m.ux));
+                        const double r1 = __builtin_fma(q1.x - m.ox, m.uy, -((q1.y - m.oy) * m.ux));
+                        const double r2 = __builtin_fma(q2.x - m.ox, m.uy, -((q2.y - m.oy) * m.ux));
+                        const double r3 = __builtin_fma(q3.x - m.ox, m.uy, -((q3.y - m.oy) * m.ux));
+                        s0 += r0 * r0;
+                        s1 += r1 * r1;
+                        s2 += r2 * r2;
+                        s3 += r3 * r3;
+                    }
+                    for (; p < N; p++) {
+                        const double r = __builtin_fma(P[p].x - m.ox, m.uy, -((P[p].y - m.oy) * m.ux));
+                        s0 += r * r;
+                    }
+                    S = (s0 + s1) + (s2 + s3);
+                }
+                tsum[k] = S;
+            }
+            __syncthreads();
+            double U = __builtin_inf();
+            for (int k = lane; k < ntied; k += 64) {
+                const double S = tsum[k];
+                if (S >= 0.0) U = fmin(U, S + tie_bound(S, N, bx.E2));
+            }
+            U = wave_min_d(U);
+            int bcnt = 0;
+            double bsum = __builtin_inf();
+            for (int kb = 0; kb < ntied && o.stop < 0; kb += 64) {
+                const int k = kb + lane;
+                bool cand = false;
+                if (k < ntied) {
+                    const double S = tsum[k];
+                    cand = S < 0.0 || S - tie_bound(S, N, bx.E2) <= U;
+                }
+                uint64_t cm = ballot(cand);
+                while (cm) {
+                    const int bit = ffs64(cm);
+                    cm &= cm - 1ull;
+                    const int t = uni(tied[kb + bit]);
+                    const Model m = model2(P[draws[2 * t]], P[draws[2 * t + 1]]);
+                    const double sum = pw_sum_lanes_any(P, N, m, vtmp, vst, nstack, lane);
+                    if (M > bcnt || (M == bcnt && sum < bsum)) {
+                        best = t;
+                        bcnt = M;
+                        bsum = sum;
+                        if (bsum <= 0.0) {
+                            o.stop = t;
+                            break;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    o = chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
+    if (B.y_proj && a.write_yproj) {
+        const double pa = rec.proj_a, pb = rec.proj_b;
+        for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
+    }
+    if (lane == 0 && B.models) B.models[c] = rec;
+}
+
 // A1: polar -> Cartesian (functions.py:59-60)
 __global__ __launch_bounds__(256) void polar_kernel(const double *__restrict__ th, const double *__restrict__ d,
                                                     double2 *__restrict__ xy, int64_t n) {
@@ -958,6 +1279,9 @@ struct lslam_ctx {
     // express-scan revolution builder scratch (per-packet flags/ranks, per-revolution info)
     void *escr;
     size_t escr_bytes;
+    // large-chunk consensus scratch: per-trial counts (+ Philox draws)
+    void *cscr;
+    size_t cscr_bytes;
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
@@ -1033,6 +1357,8 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->scr_bytes = 0;
     c->escr = nullptr;
     c->escr_bytes = 0;
+    c->cscr = nullptr;
+    c->cscr_bytes = 0;
     c->pstream = nullptr;
     c->pslot[0] = c->pslot[1] = nullptr;
     c->pslot_bytes = 0;
@@ -1081,6 +1407,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->scr) (void)hipFree(c->scr);
     if (c->escr) (void)hipFree(c->escr);
+    if (c->cscr) (void)hipFree(c->cscr);
     for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
     hipEvent_t evs[5] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call};
@@ -1470,9 +1797,15 @@ static int ensure_scratch(lslam_ctx *c, size_t bytes) {
     return LSLAM_OK;
 }
 
+// allow up to 160 KiB of LDS per workgroup (static + dynamic); a failure here must
+// not linger as the runtime's last error for the next launch check
 template <typename F>
 static void set_max_lds(F *fn) {
-    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncAttributes at;
+    size_t stat = 0;
+    if (hipFuncGetAttributes(&at, (const void *)fn) == hipSuccess) stat = at.sharedSizeBytes;
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - stat));
+    (void)hipGetLastError();
 }
 
 // Producer slot: one j per Fisher-Yates step (D * n_points entries; chunk c at
@@ -1585,12 +1918,99 @@ static void remember_outputs(lslam_ctx *c, const lslam_scan_batch *b, int T, int
         }
 }
 
+// select_kernel LDS: the chunk's points, tied trials, tie sums / inlier list, mask, sum scratch
+static int layout_select(KArgs &k, const lslam_scan_batch *b, int &lds) {
+    const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
+    const int T = k.T > 0 ? k.T : 1;
+    int off = 0;
+    k.off_pts = off; off += align16(16 * N);
+    k.off_tied = off; off += align16(4 * T);
+    k.off_tsum = off;
+    k.off_inl = off;
+    off += align16(max(8 * T, 4 * N));
+    k.off_mask = off; off += align16(N);
+    k.off_vstack = off; off += align16(8 * 24);
+    k.off_nstack = off; off += align16(4 * 72);
+    k.off_vtmp = off; off += align16(8 * 128);
+    lds = off;
+    if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk/trial sizes exceed the 160 KiB LDS");
+    return LSLAM_OK;
+}
+
+static int ensure_cscr(lslam_ctx *c, size_t bytes) {
+    if (c->cscr_bytes >= bytes) return LSLAM_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->cscr) HIPCHK(hipFree(c->cscr));
+    c->cscr = nullptr;
+    c->cscr_bytes = 0;
+    hipError_t e = hipMalloc(&c->cscr, bytes);
+    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (consensus scratch)");
+    HIPCHK(e);
+    c->cscr_bytes = bytes;
+    return LSLAM_OK;
+}
+
+// chunks of more than 128 points: count_kernel (many waves per chunk) + select_kernel
+static int launch_chunks_large(lslam_ctx *c, KArgs &k) {
+    const int T = k.T;
+    const size_t nc = (size_t)k.b.n_chunks;
+    const size_t cnt_bytes = (k.b.trial_cnt_out || T == 0) ? 0 : ((nc * T * 4 + 255) & ~(size_t)255);
+    const bool philox = k.hyp_source == LSLAM_HYP_PHILOX;
+    const size_t drw_bytes = (philox && !k.b.draws_out) ? nc * 2 * (size_t)(T + 1) * 4 : 0;
+    if (cnt_bytes + drw_bytes > 0) {
+        int st = ensure_cscr(c, cnt_bytes + drw_bytes);
+        if (st) return st;
+    }
+    k.cnt_scr = k.b.trial_cnt_out ? k.b.trial_cnt_out : (int32_t *)c->cscr;
+    if (philox) k.draws_scr = k.b.draws_out ? k.b.draws_out : (int32_t *)((unsigned char *)c->cscr + cnt_bytes);
+    const int N = k.b.max_chunk_points;
+    const int lds_cnt = align16(16 * N) + 4 * 4 * 8 + 4 * 4;
+    if (lds_cnt > 160 * 1024 - 256) return set_err(LSLAM_ERR_CAPACITY, "chunk exceeds the 160 KiB LDS");
+    int lds_sel = 0;
+    int st = layout_select(k, &k.b, lds_sel);
+    if (st) return st;
+    k.cnt_blocks = T > 0 ? (T + CNT_TRIALS_PER_WG - 1) / CNT_TRIALS_PER_WG : 0;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        set_max_lds(count_kernel<LSLAM_HYP_MT19937>);
+        set_max_lds(count_kernel<LSLAM_HYP_PHILOX>);
+        set_max_lds(count_kernel<LSLAM_HYP_EXPLICIT>);
+        set_max_lds(select_kernel<LSLAM_HYP_MT19937>);
+        set_max_lds(select_kernel<LSLAM_HYP_PHILOX>);
+        set_max_lds(select_kernel<LSLAM_HYP_EXPLICIT>);
+    });
+    if (k.cnt_blocks > 0) {
+        const dim3 grid((unsigned)(nc * k.cnt_blocks)), block(CNT_TPB);
+        switch (k.hyp_source) {
+            case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_PHILOX>, grid, block, lds_cnt, c->stream, k); break;
+            case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds_cnt, c->stream, k); break;
+            default: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_MT19937>, grid, block, lds_cnt, c->stream, k); break;
+        }
+        HIPCHK(hipGetLastError());
+    }
+    const dim3 grid((unsigned)nc), block(64);
+    switch (k.hyp_source) {
+        case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_PHILOX>, grid, block, lds_sel, c->stream, k); break;
+        case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds_sel, c->stream, k); break;
+        default: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_MT19937>, grid, block, lds_sel, c->stream, k); break;
+    }
+    HIPCHK(hipGetLastError());
+    return LSLAM_OK;
+}
+
 static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
     if (base.b.n_chunks == 0) return LSLAM_OK;
     KArgs k = base;
     k.write_yproj = write_yproj ? 1 : 0;
+    int st = timer_begin(c, LSLAM_K_CONSENSUS);
+    if (st) return st;
+    if (k.b.max_chunk_points > 128) {
+        st = launch_chunks_large(c, k);
+        if (st) return st;
+        return timer_end(c, LSLAM_K_CONSENSUS);
+    }
     int lds = 0;
-    int st = layout_chunk(k, &k.b, lds);
+    st = layout_chunk(k, &k.b, lds);
     if (st) return st;
     static std::once_flag once;
     std::call_once(once, [] {
@@ -1598,8 +2018,6 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
         set_max_lds(chunk_kernel<LSLAM_HYP_PHILOX>);
         set_max_lds(chunk_kernel<LSLAM_HYP_EXPLICIT>);
     });
-    st = timer_begin(c, LSLAM_K_CONSENSUS);
-    if (st) return st;
     const dim3 grid((unsigned)k.b.n_chunks), block(64);
     switch (k.hyp_source) {
         case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_PHILOX>, grid, block, lds, c->stream, k); break;

@@ -228,4 +228,41 @@ __device__ __forceinline__ double pw_sum_lanes(const double2 *P, int N, const Mo
     return res;
 }
 
+// pw_sum for any n with lanes over points: the leaves (<= 128 points) by
+// pw_sum_lanes, combined in numpy's recursion order (n2 = n/2 - (n/2)%8).
+// The node stack (nstack, 3*24 ints) and the partial sums (vst, 24 doubles)
+// are uniform: every lane writes and reads the same values.
+__device__ __forceinline__ double pw_sum_lanes_any(const double2 *P, int n, const Model &m, double *vtmp, double *vst,
+                                                   int *nstack, int lane) {
+    if (n <= 128) return pw_sum_lanes(P, n, m, vtmp, lane);
+    int *st_start = nstack, *st_len = nstack + 24, *st_state = nstack + 48;
+    int sp = 0, vsp = 0;
+    st_start[0] = 0; st_len[0] = n; st_state[0] = 0;
+    while (sp >= 0) {
+        const int s0 = st_start[sp], ln = st_len[sp];
+        if (ln <= 128) {
+            vst[vsp++] = pw_sum_lanes(P + s0, ln, m, vtmp, lane);
+            sp--;
+            continue;
+        }
+        int n2 = ln / 2;
+        n2 -= n2 % 8;
+        if (st_state[sp] == 0) {
+            st_state[sp] = 1;
+            sp++;
+            st_start[sp] = s0; st_len[sp] = n2; st_state[sp] = 0;
+        } else if (st_state[sp] == 1) {
+            st_state[sp] = 2;
+            sp++;
+            st_start[sp] = s0 + n2; st_len[sp] = ln - n2; st_state[sp] = 0;
+        } else {
+            const double right = vst[vsp - 1], left = vst[vsp - 2];
+            vsp -= 2;
+            vst[vsp++] = left + right;
+            sp--;
+        }
+    }
+    return vst[0];
+}
+
 }  // namespace lslam

@@ -339,20 +339,24 @@ __device__ __forceinline__ void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint
     }
 }
 
-// D uniformly distributed distinct pairs in [0, N) for chunk `chunk_id`
+// draw d of chunk `chunk_id`: a uniformly distributed distinct pair in [0, N)
+__device__ __forceinline__ void philox_pair(uint32_t N, uint32_t d, uint32_t chunk_id, uint64_t seed, int32_t &a,
+                                            int32_t &b) {
+    uint32_t c[4] = {d, chunk_id, 0x4c534c4du, 0u};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t x = (uint32_t)(((uint64_t)c[0] * N) >> 32);
+    uint32_t y = (uint32_t)(((uint64_t)c[1] * (N - 1)) >> 32);
+    if (y >= x) y += 1;
+    a = (int32_t)x;
+    b = (int32_t)y;
+}
+
+// D such pairs for chunk `chunk_id` into draws[2D]
 __device__ __forceinline__ void philox_draws(uint32_t N, uint32_t D, uint32_t chunk_id, uint64_t seed,
                                              int32_t *draws, int lane) {
     for (uint32_t d0 = 0; d0 < D; d0 += 64) {
         const uint32_t d = d0 + (uint32_t)lane;
-        if (d < D) {
-            uint32_t c[4] = {d, chunk_id, 0x4c534c4du, 0u};
-            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-            uint32_t a = (uint32_t)(((uint64_t)c[0] * N) >> 32);
-            uint32_t b = (uint32_t)(((uint64_t)c[1] * (N - 1)) >> 32);
-            if (b >= a) b += 1;
-            draws[2 * d] = (int32_t)a;
-            draws[2 * d + 1] = (int32_t)b;
-        }
+        if (d < D) philox_pair(N, d, chunk_id, seed, draws[2 * d], draws[2 * d + 1]);
     }
     __syncthreads();
 }
