@@ -76,6 +76,7 @@ struct KArgs {
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
+    double *models;     // [n_chunks][T][4] 2-point models (origin, direction)
     int cnt_blocks;     // count_kernel workgroups per chunk
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
 };
@@ -929,22 +930,26 @@ __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
 }
 
 // ------------------------------------------------------------------------
-// Large chunks (N > 128, e.g. C5: 4096 points x 2048 hypotheses).  The
+// Large chunks (N > 128, e.g. C5: 4096 points x 2048 hypotheses): the
 // count pass is split from the selection so that it can use many waves per
-// chunk with the points in LDS shared by all of them:
-//   count_kernel   workgroup = 256 lanes x CNT_HPT hypotheses of one chunk;
-//                  lanes keep their hypotheses in registers and stream the
-//                  chunk's points as LDS broadcasts (the cheap cross-product
-//                  test of chunk_consensus, two cutoffs instead of a band test;
-//                  a hypothesis with a point inside the band, a non-unit
-//                  direction or non-finite data is recounted exactly).
+// chunk:
+//   model_kernel   one lane per trial: the 2-point model (A4) -> HBM
+//   count_kernel   workgroup = one chunk x up to 1024 hypotheses; lanes hold
+//                  points in registers, the hypothesis is wave-uniform (scalar
+//                  loads, SGPR operands), so one test costs 4 FP64 ops + 2
+//                  compares and the per-hypothesis count is a scalar popcount
+//                  of the compare mask.  The cheap cross-product test of
+//                  chunk_consensus is applied as two cutoffs on |r| (no
+//                  squaring); a hypothesis with a point between them, a
+//                  non-unit direction or non-finite data is recounted exactly.
 //   select_kernel  one wave per chunk: max count, tied trials, tie brackets,
 //                  exact pairwise sums of the candidates (lanes over points),
 //                  then the same finish as chunk_kernel.
 // ------------------------------------------------------------------------
-constexpr int CNT_TPB = 256;
-constexpr int CNT_HPT = 4;
-constexpr int CNT_TRIALS_PER_WG = CNT_TPB * CNT_HPT;
+constexpr int CNT_TPB = 256;          // 4 waves
+constexpr int CNT_HYP_BLOCK = 1024;   // hypotheses per count workgroup
+
+typedef const __attribute__((address_space(4))) double cdouble_t;  // scalar-load path
 
 // bounding-box E2 and finiteness of P[0..N) (every lane gets the same values)
 struct ChunkBox {
@@ -956,13 +961,22 @@ __device__ __forceinline__ void box_partial(const double2 *src, int N, int tid, 
                                             double &xmx, double &ymn, double &ymx, bool &fin) {
     xmn = __builtin_inf(); xmx = -__builtin_inf(); ymn = __builtin_inf(); ymx = -__builtin_inf();
     fin = true;
-    for (int p = tid; p < N; p += nthr) {
-        const double2 q = src[p];
+    auto take = [&](int p, double2 q) {
         if (P) P[p] = q;
         xmn = fmin(xmn, q.x); xmx = fmax(xmx, q.x);
         ymn = fmin(ymn, q.y); ymx = fmax(ymx, q.y);
         fin = fin && (q.x - q.x == 0.0) && (q.y - q.y == 0.0);
+    };
+    int p = tid;
+    // 8 independent loads in flight per lane
+    for (; p + 7 * nthr < N; p += 8 * nthr) {
+        double2 q[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) q[j] = src[p + j * nthr];
+#pragma unroll
+        for (int j = 0; j < 8; j++) take(p + j * nthr, q[j]);
     }
+    for (; p < N; p += nthr) take(p, src[p]);
     xmn = wave_min_d(xmn); xmx = wave_max_d(xmx);
     ymn = wave_min_d(ymn); ymx = wave_max_d(ymx);
 }
@@ -987,42 +1001,82 @@ __device__ __forceinline__ void trial_pair(const KArgs &a, int c, int N, int D, 
     }
 }
 
-// exact count of one hypothesis: the cheap test where it is decisive
-__device__ __forceinline__ int exact_count(const double2 *P, int N, const Model &m, bool exact_all, double ecut,
-                                           double margin) {
-    int c = 0;
-    for (int p = 0; p < N; p++) {
-        const double2 q = P[p];
-        const double ex = q.x - m.ox, ey = q.y - m.oy;
-        const double r = __builtin_fma(ex, m.uy, -(ey * m.ux));
-        const double v = r * r;
-        bool in = v < ecut;
-        if (exact_all || fabs(v - ecut) <= margin) in = resid2(q, m) < ecut;
-        c += (int)in;
+// largest x >= 0 with fl(x*x) < e (-1 if none), smallest x with fl(x*x) > e
+__device__ __forceinline__ double sq_floor_lt(double e) {
+    if (!(e > 0.0)) return -1.0;
+    double x = sqrt(e);
+    while (x > 0.0 && x * x >= e) x = __longlong_as_double(__double_as_longlong(x) - 1);
+    for (;;) {
+        const double y = __longlong_as_double(__double_as_longlong(x) + 1);
+        if (y * y < e) x = y;
+        else break;
     }
-    return c;
+    return x;
+}
+__device__ __forceinline__ double sq_ceil_gt(double e) {
+    if (!(e >= 0.0)) return 0.0;
+    double x = sqrt(e);
+    while (x * x <= e) x = __longlong_as_double(__double_as_longlong(x) + 1);
+    for (;;) {
+        if (x == 0.0) break;
+        const double y = __longlong_as_double(__double_as_longlong(x) - 1);
+        if (y * y > e) x = y;
+        else break;
+    }
+    return x;
 }
 
+// A4 for every trial of every large chunk (and the Philox draws they use)
 template <int HYP>
-__global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
-    // dynamic LDS only (a static part would push the 160 KiB request over the limit):
-    // the chunk's points, then the per-wave box / finiteness partials
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__global__ __launch_bounds__(256) void model_kernel(const KArgs a) {
     const lslam_scan_batch &B = a.b;
-    const int c = (int)blockIdx.x / a.cnt_blocks, tb = (int)blockIdx.x % a.cnt_blocks;
-    const int tid = (int)threadIdx.x, w = tid >> 6;
+    const int T = a.T, D = T + 1;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)B.n_chunks * D) return;
+    const int c = (int)(idx / D), t = (int)(idx % D);
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
-    double2 *P = (double2 *)smem;
-    double(*s_box)[4] = (double(*)[4])(smem + ((16 * N + 15) & ~15));
-    int *s_fin = (int *)(s_box + 4);
     if (N < 3) return;
-    const int T = a.T, D = T + 1;
+    int32_t i0, i1;
+    trial_pair<HYP>(a, c, N, D, t, i0, i1);
+    if (HYP == LSLAM_HYP_PHILOX) {  // the draws select_kernel (and draws_out) read
+        a.draws_scr[((size_t)c * D + t) * 2] = i0;
+        a.draws_scr[((size_t)c * D + t) * 2 + 1] = i1;
+    }
+    if (t >= T) return;
+    const double2 *xy = (const double2 *)B.xy + p0;
+    const Model m = model2(xy[i0], xy[i1]);
+    double *o = a.models + ((size_t)c * T + t) * 4;
+    *(double4 *)o = make_double4(m.ox, m.oy, m.ux, m.uy);
+}
+
+// PPL points per lane (a tile of 256 * PPL points per pass)
+template <int PPL>
+__global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
+    __shared__ int s_lo[CNT_HYP_BLOCK], s_hi[CNT_HYP_BLOCK];
+    __shared__ uint8_t s_ex[CNT_HYP_BLOCK];
+    __shared__ double s_box[4][4];
+    __shared__ int s_fin[4];
+    const lslam_scan_batch &B = a.b;
+    const int c = (int)blockIdx.x / a.cnt_blocks;
+    const int t0 = ((int)blockIdx.x % a.cnt_blocks) * CNT_HYP_BLOCK;
+    const int tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    const int T = a.T;
+    if (N < 3 || t0 >= T) return;
+    const int nt = min(CNT_HYP_BLOCK, T - t0);
+    for (int h = tid; h < nt; h += CNT_TPB) {
+        s_lo[h] = 0;
+        s_hi[h] = 0;
+        s_ex[h] = 0;
+    }
+    const double2 *xy = (const double2 *)B.xy + p0;
     double xmn, xmx, ymn, ymx;
     bool fin;
-    box_partial((const double2 *)B.xy + p0, N, tid, CNT_TPB, P, xmn, xmx, ymn, ymx, fin);
+    box_partial(xy, N, tid, CNT_TPB, nullptr, xmn, xmx, ymn, ymx, fin);
     const bool wfin = ballot(!fin) == 0ull;
-    if ((tid & 63) == 0) {
+    if (lane == 0) {
         s_box[w][0] = xmn; s_box[w][1] = xmx; s_box[w][2] = ymn; s_box[w][3] = ymx;
         s_fin[w] = wfin;
     }
@@ -1035,67 +1089,79 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     const double ecut = a.ecut;
     const bool cheap = bx.finite && ecut < __builtin_inf();
     const double margin = (bx.E2 + ecut) * 0x1p-42;
-    const double elo = ecut - margin, ehi = ecut + margin;
-    Model m[CNT_HPT];
-    bool ex[CNT_HPT];
-    int lo[CNT_HPT], hi[CNT_HPT];
+    // c2 < ecut - margin  <=>  |r| <= r_lo;   c2 > ecut + margin  <=>  |r| >= r_hi
+    const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
+    cdouble_t *mp = (cdouble_t *)(a.models + ((size_t)c * T + t0) * 4);
+    const double nan = __builtin_nan("");
+    if (cheap) {
+        for (int tile = 0; tile < N; tile += CNT_TPB * PPL) {
+            double qx[PPL], qy[PPL];
 #pragma unroll
-    for (int h = 0; h < CNT_HPT; h++) {
-        const int t = tb * CNT_TRIALS_PER_WG + h * CNT_TPB + tid;
-        int32_t i0 = 0, i1 = 1;
-        if (t < T) {
-            trial_pair<HYP>(a, c, N, D, t, i0, i1);
-            if (HYP == LSLAM_HYP_PHILOX) {  // the draws select_kernel (and draws_out) read
-                int32_t *o = a.draws_scr + ((size_t)c * D + t) * 2;
-                o[0] = i0;
-                o[1] = i1;
+            for (int j = 0; j < PPL; j++) {
+                const int p = tile + (w * PPL + j) * 64 + lane;
+                const double2 q = p < N ? xy[p] : make_double2(nan, nan);  // NaN: neither cutoff holds
+                qx[j] = q.x;
+                qy[j] = q.y;
+            }
+            int acc_lo = 0, acc_hi = 0;  // lane k: counts of hypothesis (t & ~63) + k
+            for (int t = 0; t < nt; t++) {
+                const double ox = mp[4 * t], oy = mp[4 * t + 1], ux = mp[4 * t + 2], uy = mp[4 * t + 3];
+                uint32_t nlo = 0, nhi = 0;
+#pragma unroll
+                for (int j = 0; j < PPL; j++) {
+                    const double ex = qx[j] - ox, ey = qy[j] - oy;
+                    const double r = __builtin_fma(ex, uy, -(ey * ux));
+                    nlo += (uint32_t)popc64(ballot(fabs(r) <= r_lo));
+                    nhi += (uint32_t)popc64(ballot(fabs(r) < r_hi));
+                }
+                const bool mine = lane == (t & 63);
+                acc_lo = mine ? (int)nlo : acc_lo;
+                acc_hi = mine ? (int)nhi : acc_hi;
+                if ((t & 63) == 63 || t == nt - 1) {
+                    const int h = (t & ~63) + lane;
+                    if (h <= t) {
+                        atomicAdd(&s_lo[h], acc_lo);
+                        atomicAdd(&s_hi[h], acc_hi);
+                    }
+                    acc_lo = 0;
+                    acc_hi = 0;
+                }
             }
         }
-        m[h] = model2(P[i0], P[i1]);
-        const double un = m[h].ux * m[h].ux + m[h].uy * m[h].uy;
-        ex[h] = !cheap || !(fabs(un - 1.0) <= 0x1p-46);
-        lo[h] = 0;
-        hi[h] = 0;
     }
-    if (HYP == LSLAM_HYP_PHILOX && tb == a.cnt_blocks - 1 && tid == 0) {  // draw T: drawn, never a trial
-        int32_t i0, i1;
-        philox_pair((uint32_t)N, (uint32_t)T, (uint32_t)c, a.philox_seed, i0, i1);
-        a.draws_scr[((size_t)c * D + T) * 2] = i0;
-        a.draws_scr[((size_t)c * D + T) * 2 + 1] = i1;
+    __syncthreads();
+    // hypotheses the cutoffs cannot decide: non-unit direction (duplicate points),
+    // a point between the cutoffs, or a chunk that is not finite
+    for (int h = tid; h < nt; h += CNT_TPB) {
+        const double ux = mp[4 * h + 2], uy = mp[4 * h + 3];
+        const double un = ux * ux + uy * uy;
+        s_ex[h] = (!cheap || !(fabs(un - 1.0) <= 0x1p-46) || s_lo[h] != s_hi[h]) ? 1 : 0;
     }
-    int p = 0;
-    for (; p + 2 <= N; p += 2) {
-        const double2 q0 = P[p], q1 = P[p + 1];
-#pragma unroll
-        for (int h = 0; h < CNT_HPT; h++) {
-            const double e0x = q0.x - m[h].ox, e0y = q0.y - m[h].oy;
-            const double e1x = q1.x - m[h].ox, e1y = q1.y - m[h].oy;
-            const double r0 = __builtin_fma(e0x, m[h].uy, -(e0y * m[h].ux));
-            const double r1 = __builtin_fma(e1x, m[h].uy, -(e1y * m[h].ux));
-            const double v0 = r0 * r0, v1 = r1 * r1;
-            lo[h] += (int)(v0 < elo) + (int)(v1 < elo);
-            hi[h] += (int)(v0 <= ehi) + (int)(v1 <= ehi);
-        }
-    }
-    for (; p < N; p++) {
-        const double2 q = P[p];
-#pragma unroll
-        for (int h = 0; h < CNT_HPT; h++) {
-            const double exx = q.x - m[h].ox, eyy = q.y - m[h].oy;
-            const double r = __builtin_fma(exx, m[h].uy, -(eyy * m[h].ux));
+    __syncthreads();
+    for (int h = 0; h < nt; h++) {
+        if (!s_ex[h]) continue;  // uniform
+        Model m;
+        m.ox = mp[4 * h]; m.oy = mp[4 * h + 1]; m.ux = mp[4 * h + 2]; m.uy = mp[4 * h + 3];
+        const double un = m.ux * m.ux + m.uy * m.uy;
+        const bool exact_all = !cheap || !(fabs(un - 1.0) <= 0x1p-46);
+        int cnt = 0;
+        for (int p = tid; p < N; p += CNT_TPB) {
+            const double2 q = xy[p];
+            const double r = __builtin_fma(q.x - m.ox, m.uy, -((q.y - m.oy) * m.ux));
             const double v = r * r;
-            lo[h] += (int)(v < elo);
-            hi[h] += (int)(v <= ehi);
+            bool in = v < ecut;
+            if (exact_all || fabs(v - ecut) <= margin) in = resid2(q, m) < ecut;
+            cnt += (int)in;
         }
-    }
 #pragma unroll
-    for (int h = 0; h < CNT_HPT; h++) {
-        const int t = tb * CNT_TRIALS_PER_WG + h * CNT_TPB + tid;
-        if (t >= T) continue;
-        int cnt = lo[h];
-        if (ex[h] || lo[h] != hi[h]) cnt = exact_count(P, N, m[h], ex[h], ecut, margin);  // rare
-        a.cnt_scr[(size_t)c * T + t] = cnt;
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        __syncthreads();
+        if (tid == 0) s_lo[h] = 0;
+        __syncthreads();
+        if (lane == 0) atomicAdd(&s_lo[h], cnt);
+        __syncthreads();
     }
+    for (int h = tid; h < nt; h += CNT_TPB) a.cnt_scr[(size_t)c * T + t0 + h] = s_lo[h];
 }
 
 template <int HYP>
@@ -1147,7 +1213,21 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
     __syncthreads();
     const double ecut = a.ecut;
     const bool cheap = bx.finite && ecut < __builtin_inf();
-    const int32_t *cnt = a.cnt_scr + (size_t)c * T;
+    // the chunk's per-trial counts -> LDS (many loads in flight), then the max
+    int32_t *cnt = (int32_t *)(smem + a.off_cnt);
+    {
+        const int32_t *g = a.cnt_scr + (size_t)c * T;
+        int t = lane;
+        for (; t + 7 * 64 < T; t += 8 * 64) {
+            int32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = g[t + j * 64];
+#pragma unroll
+            for (int j = 0; j < 8; j++) cnt[t + j * 64] = v[j];
+        }
+        for (; t < T; t += 64) cnt[t] = g[t];
+    }
+    __syncthreads();
     int M = 0;
     for (int t = lane; t < T; t += 64) M = max(M, cnt[t]);
     M = uni(wave_max(M));
@@ -1173,33 +1253,31 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
         if (!need_sums) {
             best = tied[0];
         } else {
-            // brackets of the tied trials' sums (-1: always a candidate)
-            for (int k = lane; k < ntied; k += 64) {
-                const int t = tied[k];
+            // brackets of the tied trials' sums (-1: always a candidate): one tied
+            // trial at a time, lanes over points (any summation order is covered
+            // by tie_bound)
+            for (int k = 0; k < ntied; k++) {
+                const int t = uni(tied[k]);
                 const Model m = model2(P[draws[2 * t]], P[draws[2 * t + 1]]);
                 const double un = m.ux * m.ux + m.uy * m.uy;
                 double S = -1.0;
                 if (cheap && fabs(un - 1.0) <= 0x1p-46) {
-                    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-                    int p = 0;
-                    for (; p + 4 <= N; p += 4) {
-                        const double2 q0 = P[p], q1 = P[p + 1], q2 = P[p + 2], q3 = P[p + 3];
+                    double s0 = 0.0, s1 = 0.0;
+                    int p = lane;
+                    for (; p + 64 < N; p += 128) {
+                        const double2 q0 = P[p], q1 = P[p + 64];
                         const double r0 = __builtin_fma(q0.x - m.ox, m.uy, -((q0.y - m.oy) * m.ux));
                         const double r1 = __builtin_fma(q1.x - m.ox, m.uy, -((q1.y - m.oy) * m.ux));
-                        const double r2 = __builtin_fma(q2.x - m.ox, m.uy, -((q2.y - m.oy) * m.ux));
-                        const double r3 = __builtin_fma(q3.x - m.ox, m.uy, -((q3.y - m.oy) * m.ux));
                         s0 += r0 * r0;
                         s1 += r1 * r1;
-                        s2 += r2 * r2;
-                        s3 += r3 * r3;
                     }
-                    for (; p < N; p++) {
+                    if (p < N) {
                         const double r = __builtin_fma(P[p].x - m.ox, m.uy, -((P[p].y - m.oy) * m.ux));
                         s0 += r * r;
                     }
-                    S = (s0 + s1) + (s2 + s3);
+                    S = unid(wave_sum(s0 + s1));
                 }
-                tsum[k] = S;
+                if (lane == 0) tsum[k] = S;
             }
             __syncthreads();
             double U = __builtin_inf();
@@ -1925,6 +2003,7 @@ static int layout_select(KArgs &k, const lslam_scan_batch *b, int &lds) {
     int off = 0;
     k.off_pts = off; off += align16(16 * N);
     k.off_tied = off; off += align16(4 * T);
+    k.off_cnt = off; off += align16(4 * T);
     k.off_tsum = off;
     k.off_inl = off;
     off += align16(max(8 * T, 4 * N));
@@ -1956,43 +2035,48 @@ static int launch_chunks_large(lslam_ctx *c, KArgs &k) {
     const size_t nc = (size_t)k.b.n_chunks;
     const size_t cnt_bytes = (k.b.trial_cnt_out || T == 0) ? 0 : ((nc * T * 4 + 255) & ~(size_t)255);
     const bool philox = k.hyp_source == LSLAM_HYP_PHILOX;
-    const size_t drw_bytes = (philox && !k.b.draws_out) ? nc * 2 * (size_t)(T + 1) * 4 : 0;
-    if (cnt_bytes + drw_bytes > 0) {
-        int st = ensure_cscr(c, cnt_bytes + drw_bytes);
-        if (st) return st;
-    }
-    k.cnt_scr = k.b.trial_cnt_out ? k.b.trial_cnt_out : (int32_t *)c->cscr;
-    if (philox) k.draws_scr = k.b.draws_out ? k.b.draws_out : (int32_t *)((unsigned char *)c->cscr + cnt_bytes);
-    const int N = k.b.max_chunk_points;
-    const int lds_cnt = align16(16 * N) + 4 * 4 * 8 + 4 * 4;
-    if (lds_cnt > 160 * 1024 - 256) return set_err(LSLAM_ERR_CAPACITY, "chunk exceeds the 160 KiB LDS");
-    int lds_sel = 0;
-    int st = layout_select(k, &k.b, lds_sel);
+    const size_t drw_bytes = (philox && !k.b.draws_out) ? ((nc * 2 * (size_t)(T + 1) * 4 + 255) & ~(size_t)255) : 0;
+    const size_t mdl_bytes = nc * (size_t)(T > 0 ? T : 1) * 32;
+    int st = ensure_cscr(c, cnt_bytes + drw_bytes + mdl_bytes);
     if (st) return st;
-    k.cnt_blocks = T > 0 ? (T + CNT_TRIALS_PER_WG - 1) / CNT_TRIALS_PER_WG : 0;
+    unsigned char *base = (unsigned char *)c->cscr;
+    k.cnt_scr = k.b.trial_cnt_out ? k.b.trial_cnt_out : (int32_t *)base;
+    if (philox) k.draws_scr = k.b.draws_out ? k.b.draws_out : (int32_t *)(base + cnt_bytes);
+    k.models = (double *)(base + cnt_bytes + drw_bytes);
+    const int N = k.b.max_chunk_points;
+    int lds_sel = 0;
+    st = layout_select(k, &k.b, lds_sel);
+    if (st) return st;
+    k.cnt_blocks = T > 0 ? (T + CNT_HYP_BLOCK - 1) / CNT_HYP_BLOCK : 0;
     static std::once_flag once;
     std::call_once(once, [] {
-        set_max_lds(count_kernel<LSLAM_HYP_MT19937>);
-        set_max_lds(count_kernel<LSLAM_HYP_PHILOX>);
-        set_max_lds(count_kernel<LSLAM_HYP_EXPLICIT>);
         set_max_lds(select_kernel<LSLAM_HYP_MT19937>);
         set_max_lds(select_kernel<LSLAM_HYP_PHILOX>);
         set_max_lds(select_kernel<LSLAM_HYP_EXPLICIT>);
     });
+    const size_t nmod = nc * (size_t)(T + 1);
+    const dim3 mgrid((unsigned)((nmod + 255) / 256)), block(256);
+    switch (k.hyp_source) {
+        case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(model_kernel<LSLAM_HYP_PHILOX>, mgrid, block, 0, c->stream, k); break;
+        case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(model_kernel<LSLAM_HYP_EXPLICIT>, mgrid, block, 0, c->stream, k); break;
+        default: hipLaunchKernelGGL(model_kernel<LSLAM_HYP_MT19937>, mgrid, block, 0, c->stream, k); break;
+    }
+    HIPCHK(hipGetLastError());
     if (k.cnt_blocks > 0) {
-        const dim3 grid((unsigned)(nc * k.cnt_blocks)), block(CNT_TPB);
-        switch (k.hyp_source) {
-            case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_PHILOX>, grid, block, lds_cnt, c->stream, k); break;
-            case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds_cnt, c->stream, k); break;
-            default: hipLaunchKernelGGL(count_kernel<LSLAM_HYP_MT19937>, grid, block, lds_cnt, c->stream, k); break;
-        }
+        const dim3 grid((unsigned)(nc * k.cnt_blocks)), cblock(CNT_TPB);
+        // points per lane: the smallest power of two covering the chunk, at most 16 (then tiles)
+        if (N <= 256) hipLaunchKernelGGL(count_kernel<1>, grid, cblock, 0, c->stream, k);
+        else if (N <= 512) hipLaunchKernelGGL(count_kernel<2>, grid, cblock, 0, c->stream, k);
+        else if (N <= 1024) hipLaunchKernelGGL(count_kernel<4>, grid, cblock, 0, c->stream, k);
+        else if (N <= 2048) hipLaunchKernelGGL(count_kernel<8>, grid, cblock, 0, c->stream, k);
+        else hipLaunchKernelGGL(count_kernel<16>, grid, cblock, 0, c->stream, k);
         HIPCHK(hipGetLastError());
     }
-    const dim3 grid((unsigned)nc), block(64);
+    const dim3 grid((unsigned)nc), sblock(64);
     switch (k.hyp_source) {
-        case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_PHILOX>, grid, block, lds_sel, c->stream, k); break;
-        case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds_sel, c->stream, k); break;
-        default: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_MT19937>, grid, block, lds_sel, c->stream, k); break;
+        case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_PHILOX>, grid, sblock, lds_sel, c->stream, k); break;
+        case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_EXPLICIT>, grid, sblock, lds_sel, c->stream, k); break;
+        default: hipLaunchKernelGGL(select_kernel<LSLAM_HYP_MT19937>, grid, sblock, lds_sel, c->stream, k); break;
     }
     HIPCHK(hipGetLastError());
     return LSLAM_OK;
