@@ -360,9 +360,25 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
                 if (S >= 0.0) U = fmin(U, S + tie_bound(S, N, E2));
             }
             U = wave_min_d(U);
+            // a single candidate wins without its exact sum unless the stop test
+            // (sum == 0, only possible with M == N) could fire
+            int ncand = 0, cand1 = -1;
+            for (int kb = 0; kb < ntied; kb += 64) {
+                const int k = kb + lane;
+                bool cand = false;
+                if (k < ntied) {
+                    const double S = tsum[tied[k]];
+                    cand = S < 0.0 || S - tie_bound(S, N, E2) <= U;
+                }
+                const uint64_t cm = ballot(cand);
+                if (cm && cand1 < 0) cand1 = kb + ffs64(cm);
+                ncand += popc64(cm);
+            }
+            const bool lone = ncand == 1 && M < N && ecut > 0.0;
+            if (lone) best = uni(tied[cand1]);
             int bcnt = 0;
             double bsum = __builtin_inf();
-            for (int kb = 0; kb < ntied && o.stop < 0; kb += 64) {
+            for (int kb = 0; !lone && kb < ntied && o.stop < 0; kb += 64) {
                 const int k = kb + lane;
                 bool cand = false;
                 if (k < ntied) {
@@ -1088,7 +1104,14 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     const ChunkBox bx = box_finish(xmn, xmx, ymn, ymx, s_fin[0] && s_fin[1] && s_fin[2] && s_fin[3]);
     const double ecut = a.ecut;
     const bool cheap = bx.finite && ecut < __builtin_inf();
-    const double margin = (bx.E2 + ecut) * 0x1p-42;
+    // The main loop evaluates the cross product as r = fl(fl(x uy - y ux) - k),
+    // k = fl(ox uy - oy ux) per hypothesis: 3 FP64 ops instead of 4.  Against
+    // chunk_consensus's fl(ex uy - ey ux) this adds at most ~8 u R |r| to r^2
+    // (R = max|x| + max|y| over the chunk box, which holds o), so the band
+    // gets an R sqrt(ecut) term; 2^-42 leaves a factor 2^8 of slack on it as on
+    // the E2 term.  Outside the band the cheap test decides as before.
+    const double Rb = fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx));
+    const double margin = (bx.E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
     // c2 < ecut - margin  <=>  |r| <= r_lo;   c2 > ecut + margin  <=>  |r| >= r_hi
     const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
     cdouble_t *mp = (cdouble_t *)(a.models + ((size_t)c * T + t0) * 4);
@@ -1104,13 +1127,17 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
                 qy[j] = q.y;
             }
             int acc_lo = 0, acc_hi = 0;  // lane k: counts of hypothesis (t & ~63) + k
+            double nox = mp[0], noy = mp[1], nux = mp[2], nuy = mp[3];
             for (int t = 0; t < nt; t++) {
-                const double ox = mp[4 * t], oy = mp[4 * t + 1], ux = mp[4 * t + 2], uy = mp[4 * t + 3];
+                const double ox = nox, oy = noy, ux = nux, uy = nuy;
+                if (t + 1 < nt) {  // next hypothesis' scalar loads in flight during this one
+                    nox = mp[4 * t + 4]; noy = mp[4 * t + 5]; nux = mp[4 * t + 6]; nuy = mp[4 * t + 7];
+                }
+                const double k = __builtin_fma(ox, uy, -(oy * ux));
                 uint32_t nlo = 0, nhi = 0;
 #pragma unroll
                 for (int j = 0; j < PPL; j++) {
-                    const double ex = qx[j] - ox, ey = qy[j] - oy;
-                    const double r = __builtin_fma(ex, uy, -(ey * ux));
+                    const double r = __builtin_fma(qx[j], uy, -(qy[j] * ux)) - k;
                     nlo += (uint32_t)popc64(ballot(fabs(r) <= r_lo));
                     nhi += (uint32_t)popc64(ballot(fabs(r) < r_hi));
                 }
@@ -1138,8 +1165,12 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
         s_ex[h] = (!cheap || !(fabs(un - 1.0) <= 0x1p-46) || s_lo[h] != s_hi[h]) ? 1 : 0;
     }
     __syncthreads();
-    for (int h = 0; h < nt; h++) {
-        if (!s_ex[h]) continue;  // uniform
+    for (int hb = 0; hb < nt; hb += 64) {
+      // the flagged hypotheses of this group of 64, one ballot instead of 64 LDS round trips
+      uint64_t fm = ballot(hb + lane < nt && s_ex[hb + lane] != 0);
+      while (fm) {
+        const int h = hb + ffs64(fm);
+        fm &= fm - 1ull;
         Model m;
         m.ox = mp[4 * h]; m.oy = mp[4 * h + 1]; m.ux = mp[4 * h + 2]; m.uy = mp[4 * h + 3];
         const double un = m.ux * m.ux + m.uy * m.uy;
@@ -1160,9 +1191,22 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
         __syncthreads();
         if (lane == 0) atomicAdd(&s_lo[h], cnt);
         __syncthreads();
+      }
     }
     for (int h = tid; h < nt; h += CNT_TPB) a.cnt_scr[(size_t)c * T + t0 + h] = s_lo[h];
 }
+
+// diagnostic build only: select_kernel phase cycles into dbg[c][8 + k]
+#ifdef LSLAM_STAMPS
+#define SEL_STAMP(k)                                                         \
+    do {                                                                     \
+        const uint64_t _t = lslam_stamp();                                   \
+        if (a.dbg && lane == 0) a.dbg[(size_t)c * 16 + 8 + (k)] += _t - _sel_prev; \
+        _sel_prev = _t;                                                      \
+    } while (0)
+#else
+#define SEL_STAMP(k) do {} while (0)
+#endif
 
 template <int HYP>
 __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
@@ -1203,12 +1247,16 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
         }
         return;
     }
+#ifdef LSLAM_STAMPS
+    uint64_t _sel_prev = lslam_stamp();
+#endif
     const int32_t *draws = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
     if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
         for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
     double xmn, xmx, ymn, ymx;
     bool fin;
     box_partial((const double2 *)B.xy + p0, N, lane, 64, P, xmn, xmx, ymn, ymx, fin);
+    SEL_STAMP(0);
     const ChunkBox bx = box_finish(unid(xmn), unid(xmx), unid(ymn), unid(ymx), ballot(!fin) == 0ull);
     __syncthreads();
     const double ecut = a.ecut;
@@ -1240,6 +1288,7 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
         ntied += popc64(bm);
     }
     __syncthreads();
+    SEL_STAMP(1);
     ChunkOut o;
     o.flags = 0;
     o.best = -1;
@@ -1280,15 +1329,32 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
                 if (lane == 0) tsum[k] = S;
             }
             __syncthreads();
+            SEL_STAMP(2);
             double U = __builtin_inf();
             for (int k = lane; k < ntied; k += 64) {
                 const double S = tsum[k];
                 if (S >= 0.0) U = fmin(U, S + tie_bound(S, N, bx.E2));
             }
             U = wave_min_d(U);
+            // a single candidate wins without its exact sum unless the stop test
+            // (sum == 0, only possible with M == N) could fire
+            int ncand = 0, cand1 = -1;
+            for (int kb = 0; kb < ntied; kb += 64) {
+                const int k = kb + lane;
+                bool cand = false;
+                if (k < ntied) {
+                    const double S = tsum[k];
+                    cand = S < 0.0 || S - tie_bound(S, N, bx.E2) <= U;
+                }
+                const uint64_t cm = ballot(cand);
+                if (cm && cand1 < 0) cand1 = kb + ffs64(cm);
+                ncand += popc64(cm);
+            }
+            const bool lone = ncand == 1 && M < N && ecut > 0.0;
+            if (lone) best = uni(tied[cand1]);
             int bcnt = 0;
             double bsum = __builtin_inf();
-            for (int kb = 0; kb < ntied && o.stop < 0; kb += 64) {
+            for (int kb = 0; !lone && kb < ntied && o.stop < 0; kb += 64) {
                 const int k = kb + lane;
                 bool cand = false;
                 if (k < ntied) {
@@ -1315,13 +1381,22 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
             }
         }
     }
+    SEL_STAMP(3);
     o = chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    SEL_STAMP(4);
     const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
     if (B.y_proj && a.write_yproj) {
         const double pa = rec.proj_a, pb = rec.proj_b;
         for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
     }
     if (lane == 0 && B.models) B.models[c] = rec;
+    SEL_STAMP(5);
+#ifdef LSLAM_STAMPS
+    if (a.dbg && lane == 0) {
+        a.dbg[(size_t)c * 16 + 14] += (uint64_t)ntied;
+        a.dbg[(size_t)c * 16 + 15] += (uint64_t)o.n_inl;
+    }
+#endif
 }
 
 // A1: polar -> Cartesian (functions.py:59-60)

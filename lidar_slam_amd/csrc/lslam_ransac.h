@@ -160,25 +160,23 @@ __device__ __forceinline__ double wave_max_d(double v) {
 // restates this order.
 __device__ __forceinline__ Model refit_line(const double2 *P, const int32_t *inl, int nin, int lane) {
     Model f;
-    double sx, sy;
-    {
-        const double2 q = P[inl[0]];
-        sx = q.x;
-        sy = q.y;
-    }
+    // The two sequential sums run side by side: even lanes accumulate x, odd
+    // lanes y (same additions, same order), so one v_add per inlier carries
+    // both chains and the gathers of the next inliers stay off the chain.
+    const double *Pc = (const double *)P;
+    const int comp = lane & 1;
+    double acc = Pc[2 * inl[0] + comp];
     int i = 1;
-    for (; i + 4 <= nin; i += 4) {
-        const double2 q0 = P[inl[i]], q1 = P[inl[i + 1]], q2 = P[inl[i + 2]], q3 = P[inl[i + 3]];
-        sx += q0.x; sy += q0.y;
-        sx += q1.x; sy += q1.y;
-        sx += q2.x; sy += q2.y;
-        sx += q3.x; sy += q3.y;
+    for (; i + 8 <= nin; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = Pc[2 * inl[i + j] + comp];
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc += v[j];
     }
-    for (; i < nin; i++) {
-        const double2 q = P[inl[i]];
-        sx += q.x;
-        sy += q.y;
-    }
+    for (; i < nin; i++) acc += Pc[2 * inl[i] + comp];
+    const double sx = unid(acc);                      // lane 0
+    const double sy = __shfl(acc, 1);                 // lane 1
     f.ox = sx / (double)nin;
     f.oy = sy / (double)nin;
     double sxx = 0.0, sxy = 0.0, syy = 0.0;

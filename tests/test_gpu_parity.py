@@ -321,8 +321,24 @@ def _border_batch():
     return chunks
 
 
-def test_border_band_and_degenerate_hypotheses(ctx):
-    chunks = _border_batch()
+def _border_batch_large():
+    """The border chunks grown past 128 points (the count/select kernels): copies
+    shifted along each chunk's own line keep the threshold distances; chunk 3
+    repeats its duplicates."""
+    c = _border_batch()
+    along = [(60.0, 0.0), (0.0, 60.0), None, (30.0, 60.0), (60.0, 30.0), (60.0, 0.0), (-60.0, 0.0)]
+    out = []
+    for ch, v in zip(c, along):
+        reps = [ch + (0.0 if v is None else np.array(v) * k) for k in range(5)]
+        out.append(np.concatenate(reps))
+    return out
+
+
+@pytest.mark.parametrize("large", [False, True])
+def test_border_band_and_degenerate_hypotheses(ctx, large):
+    chunks = _border_batch_large() if large else _border_batch()
+    if large:
+        assert min(len(ch) for ch in chunks) > 128
     seeds = np.arange(40, dtype=np.uint32) * 7919 + 11
     S = len(seeds)
     xy = np.concatenate([np.concatenate(chunks)] * S)
