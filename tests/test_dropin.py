@@ -106,3 +106,71 @@ def test_system_ukf_vs_oracle():
     f.update(z, lm)
     assert np.max(np.abs(sysm.ukf.x - f.x)) < 1e-4
     assert np.max(np.abs(sysm.ukf.P - f.P)) < 1e-6
+
+
+@pytest.mark.gpu
+def test_revolution_dispatcher_replays_live_reference_run(golden):
+    """The live fixture's 112 chunks grouped into revolutions of 8 and run one
+    launch per revolution (process_revolution) end in the reference's RNG
+    state, landmark list and projected points after every revolution."""
+    g = golden("live.npz")
+    np.random.seed(int(g["seed"][0]))
+    landmarks = []
+    number = 0
+    C = len(g["a"])
+    for r0 in range(0, C, 8):
+        cs = range(r0, min(r0 + 8, C))
+        chunks = [g["xy"][g["chunk_pt_off"][c]:g["chunk_pt_off"][c + 1]] for c in cs]
+        pts, number = ransac_functions.process_revolution(chunks, number, landmarks)
+        last = cs[-1]
+        st = np.random.get_state()
+        assert np.array_equal(st[1], g["state_after_key"][last]) and st[2] == g["state_after_pos"][last]
+        q0, q1 = g["q_off"][cs[0]], g["q_off"][last + 1]
+        assert len(pts) == q1 - q0
+        assert list(pts.x) == list(g["q_x"][q0:q1])
+        assert np.allclose(pts.y, g["q_y"][q0:q1], rtol=1e-9, atol=1e-9)
+        assert [p.x() for p in pts[:3]] == list(g["q_x"][q0:q0 + 3])
+        l0, l1 = g["lm_off"][last], g["lm_off"][last + 1]
+        assert [L.id for L in landmarks] == list(g["lm_id"][l0:l1])
+        assert [L.life for L in landmarks] == list(g["lm_life"][l0:l1])
+    assert number == C
+
+
+@pytest.mark.gpu
+def test_revolution_dispatcher_thread_and_error_replay():
+    import threading
+    import time as _t
+    rng = np.random.default_rng(4)
+    line = lambda n, s: np.stack([np.arange(n) * 10.0, s * np.arange(n) * 10.0 + rng.normal(0, 2, n)], 1)
+    pts, pairs, allp, temp, lms = [], [], [], [], []
+    ev, stop = threading.Event(), threading.Event()
+    th = threading.Thread(target=ransac_functions.check_ransac_revolution,
+                          args=(pairs, temp, allp, pts, lms, ev), kwargs={"stop": stop})
+    np.random.seed(9)
+    th.start()
+    chunks = [line(100, 0.5), line(100, -1.0), line(20, 2.0)]
+    for c in chunks:
+        temp.append(c)
+        pts.append(c.tolist())
+    pts.append(0)
+    t0 = _t.time()
+    while not ev.is_set() and _t.time() - t0 < 60:
+        _t.sleep(0.01)
+    stop.set()
+    th.join(10)
+    assert ev.is_set() and len(pairs) == 1 and len(allp) == 1
+    assert len(allp[0]) == 220 and len(pairs[0]) > 0
+    # the per-chunk path from the same state gives the same points and list
+    np.random.seed(9)
+    lm2, q_all, n = [], [], 0
+    for c in chunks:
+        q, f, new = ransac_functions.landmark_extraction([c.tolist()], n, lm2)
+        q_all += q
+        if new:
+            lm2.append(f)
+        n += 1
+    assert [p.x() for p in q_all] == list(pairs[0].x)
+    assert [(L.id, L.life) for L in lm2] == [(L.id, L.life) for L in lms]
+    # a 2-point chunk raises ValueError at that chunk, as in the reference
+    with pytest.raises(ValueError):
+        ransac_functions.process_revolution([line(50, 1.0), line(2, 1.0)], 0, [])
