@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <atomic>
 #include <mutex>
@@ -72,6 +73,7 @@ struct KArgs {
     int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
     uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
+    int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     // large chunks (N > 128): count_kernel -> select_kernel
@@ -250,6 +252,12 @@ __device__ __forceinline__ double tie_bound(double S, int N, double E2) {
     return ((double)N * E2 + (double)(N + 32) * S) * 0x1p-42;
 }
 
+// the same for sums of the reassociated cross product (chunk_consensus): each
+// term may further differ by ~8 u R |r| <= 8 u R sqrt(E2)
+__device__ __forceinline__ double tie_bound_r(double S, int N, double E2, double R) {
+    return ((double)N * (E2 + R * (sqrt(E2) + 1.0)) + (double)(N + 32) * S) * 0x1p-42;
+}
+
 __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *cnt,
                                     int32_t *tied, double *tsum, int32_t *inl, double *vtmp, double *vstack,
                                     int *nstack, int32_t *cnt_out, int lane) {
@@ -284,7 +292,14 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
     o.n_inl = 0;
     o.last_inl = -1;
     o.n_draws = T + 1;
-    const double margin = (E2 + ecut) * 0x1p-42;
+    // Reassociated cross product r = fl(fl(x uy - y ux) - k), k = ox uy - oy ux
+    // per hypothesis, with the band widened by the R sqrt(ecut) term (see
+    // count_kernel) and tested as two cutoffs on |r|: 3 FP64 ops + S + two
+    // counts per evaluation.  A lane whose counts differ (a point in the band)
+    // or whose direction is not unit recounts exactly.
+    const double Rb = unid(fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx)));
+    const double margin = (E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
+    const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
     int M = 0;
     for (int tb = 0; tb < T; tb += 64) {
         const int t = tb + lane;
@@ -292,42 +307,36 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         const Model m = model2(P[draws[2 * tt]], P[draws[2 * tt + 1]]);
         const double un = m.ux * m.ux + m.uy * m.uy;
         const bool exact_all = !(fabs(un - 1.0) <= 0x1p-46);
-        int c = 0;
+        const double k = __builtin_fma(m.ox, m.uy, -(m.oy * m.ux));
+        int lo = 0, hi = 0;
         double S = 0.0;
         int p = 0;
-        for (; p + 4 <= N; p += 4) {
-            const double2 q0 = P[p], q1 = P[p + 1], q2 = P[p + 2], q3 = P[p + 3];
-            const double e0x = q0.x - m.ox, e0y = q0.y - m.oy, e1x = q1.x - m.ox, e1y = q1.y - m.oy;
-            const double e2x = q2.x - m.ox, e2y = q2.y - m.oy, e3x = q3.x - m.ox, e3y = q3.y - m.oy;
-            const double r0 = __builtin_fma(e0x, m.uy, -(e0y * m.ux));
-            const double r1 = __builtin_fma(e1x, m.uy, -(e1y * m.ux));
-            const double r2 = __builtin_fma(e2x, m.uy, -(e2y * m.ux));
-            const double r3 = __builtin_fma(e3x, m.uy, -(e3y * m.ux));
-            const double v0 = r0 * r0, v1 = r1 * r1, v2 = r2 * r2, v3 = r3 * r3;
-            S += v0;
-            S += v1;
-            S += v2;
-            S += v3;
-            bool i0 = v0 < ecut, i1 = v1 < ecut, i2 = v2 < ecut, i3 = v3 < ecut;
-            const bool b0 = fabs(v0 - ecut) <= margin, b1 = fabs(v1 - ecut) <= margin;
-            const bool b2 = fabs(v2 - ecut) <= margin, b3 = fabs(v3 - ecut) <= margin;
-            if (ballot(exact_all || b0 || b1 || b2 || b3) != 0ull) {
-                if (exact_all || b0) i0 = resid2(q0, m) < ecut;
-                if (exact_all || b1) i1 = resid2(q1, m) < ecut;
-                if (exact_all || b2) i2 = resid2(q2, m) < ecut;
-                if (exact_all || b3) i3 = resid2(q3, m) < ecut;
-            }
-            c += (int)i0 + (int)i1 + (int)i2 + (int)i3;
+        for (; p + 2 <= N; p += 2) {
+            const double2 q0 = P[p], q1 = P[p + 1];
+            const double r0 = __builtin_fma(q0.x, m.uy, -(q0.y * m.ux)) - k;
+            const double r1 = __builtin_fma(q1.x, m.uy, -(q1.y * m.ux)) - k;
+            S = __builtin_fma(r0, r0, S);
+            S = __builtin_fma(r1, r1, S);
+            lo += (int)(fabs(r0) <= r_lo) + (int)(fabs(r1) <= r_lo);
+            hi += (int)(fabs(r0) < r_hi) + (int)(fabs(r1) < r_hi);
         }
-        for (; p < N; p++) {
+        if (p < N) {
             const double2 q = P[p];
-            const double ex = q.x - m.ox, ey = q.y - m.oy;
-            const double r = __builtin_fma(ex, m.uy, -(ey * m.ux));
-            const double v = r * r;
-            S += v;
-            bool in = v < ecut;
-            if (exact_all || fabs(v - ecut) <= margin) in = resid2(q, m) < ecut;
-            c += (int)in;
+            const double r = __builtin_fma(q.x, m.uy, -(q.y * m.ux)) - k;
+            S = __builtin_fma(r, r, S);
+            lo += (int)(fabs(r) <= r_lo);
+            hi += (int)(fabs(r) < r_hi);
+        }
+        int c = lo;
+        if (exact_all || lo != hi) {  // rare: lane-divergent exact recount
+            c = 0;
+            for (int q = 0; q < N; q++) {
+                const double r = __builtin_fma(P[q].x, m.uy, -(P[q].y * m.ux)) - k;
+                const double v = r * r;
+                bool in = v < ecut;
+                if (exact_all || fabs(v - ecut) <= margin) in = resid2(P[q], m) < ecut;
+                c += (int)in;
+            }
         }
         if (t < T) {
             cnt[t] = c;
@@ -357,7 +366,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
             double U = __builtin_inf();
             for (int k = lane; k < ntied; k += 64) {
                 const double S = tsum[tied[k]];
-                if (S >= 0.0) U = fmin(U, S + tie_bound(S, N, E2));
+                if (S >= 0.0) U = fmin(U, S + tie_bound_r(S, N, E2, Rb));
             }
             U = wave_min_d(U);
             // a single candidate wins without its exact sum unless the stop test
@@ -368,7 +377,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
                 bool cand = false;
                 if (k < ntied) {
                     const double S = tsum[tied[k]];
-                    cand = S < 0.0 || S - tie_bound(S, N, E2) <= U;
+                    cand = S < 0.0 || S - tie_bound_r(S, N, E2, Rb) <= U;
                 }
                 const uint64_t cm = ballot(cand);
                 if (cm && cand1 < 0) cand1 = kb + ffs64(cm);
@@ -383,7 +392,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
                 bool cand = false;
                 if (k < ntied) {
                     const double S = tsum[tied[k]];
-                    cand = S < 0.0 || S - tie_bound(S, N, E2) <= U;
+                    cand = S < 0.0 || S - tie_bound_r(S, N, E2, Rb) <= U;
                 }
                 uint64_t cm = ballot(cand);
                 while (cm) {
@@ -542,9 +551,7 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
 // the scan kernel
 // ------------------------------------------------------------------------
 template <int HYP, int MODE>
-__global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int s = blockIdx.x;
+__device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned char *smem) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
 
@@ -769,41 +776,65 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         }
     }
 }
+// Consumer kernels loop over their items with a grid capped at a few waves per
+// CU (launch_cap): they then fill the issue slots the producer's chains leave
+// idle instead of competing with them for residency (which made the producer's
+// placement, and so the step time, vary from run to run).
+template <int HYP, int MODE>
+__global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
+        scan_body<HYP, MODE>(a, s, smem);
+        __syncthreads();
+    }
+}
 
 // ------------------------------------------------------------------------
 // rng_kernel: the chained parity stream of one scan -> every chunk's draws
 // (wave 0 parses, wave 1 twists ahead and resolves; lslam_rng_pipe.h)
 // ------------------------------------------------------------------------
-template <typename JT>
-__global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
+// PPW parser waves (one scan each) + one helper wave per workgroup.  One helper
+// twists for all PPW parsers (it is asleep most of the time), so a 4096-scan
+// batch holds 5 waves per SIMD instead of 8: the producer no longer needs every
+// wave slot of the chip, and the previous call's consumers run beside it
+// without holding back any of its workgroups.
+template <typename JT, int PPW>
+__global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int s = blockIdx.x;
     const int lane = (int)threadIdx.x & 63;
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
-    RngPipe rp;
-    rp.blk = (uint32_t *)(smem + a.off_blk);
-    rp.fl = (lds_flag_t *)(smem + a.off_fl);
-#ifdef LSLAM_STAMPS
-    for (int k = 0; k < 8; k++) rp.acc[k] = 0;
-    const uint64_t t_start = lslam_stamp();
-    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
     const uint32_t D = (uint32_t)a.T + 1u;
-    if (wave == 1) {
-        // block 0 = the initial state (raw)
-        if (B.mt_state_in) {
-            const uint32_t *src = B.mt_state_in + (size_t)s * 625;
-            for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
-        } else {
-            mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
+    auto pipe_of = [&](int j) {
+        RngPipe rp;
+        unsigned char *base = smem + (size_t)j * a.rng_pipe_bytes;
+        rp.blk = (uint32_t *)(base + a.off_blk);
+        rp.fl = (lds_flag_t *)(base + a.off_fl);
+        return rp;
+    };
+    if (wave < PPW) {
+        const int s = (int)blockIdx.x * PPW + wave;
+        RngPipe rp = pipe_of(wave);
+#ifdef LSLAM_STAMPS
+        for (int k = 0; k < 8; k++) rp.acc[k] = 0;
+        const uint64_t t_start = lslam_stamp();
+        const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+        // block 0 = the initial state (raw); flags
+        if (s < B.n_scans) {
+            if (B.mt_state_in) {
+                const uint32_t *src = B.mt_state_in + (size_t)s * 625;
+                for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
+            } else {
+                mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
+            }
         }
         if (lane < F_NFLAGS) rp.fl[lane] = 0;
-    }
-    __syncthreads();
-    if (wave == 0) {
+        if (s >= B.n_scans && lane == 0) rp.fl[F_BLKUSE] = -1;  // no scan: nothing to twist
+        __syncthreads();
+        if (s >= B.n_scans) return;
         // ---- parser: its chain is the kernel's critical path
+        const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
         rp.total_steps = 0;
         rp.done_steps = 0;
         for (int c = c0; c < c1; c++) {
@@ -823,7 +854,7 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
             if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
             else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
         }
-        lds_flag_put(rp.fl + F_BLKUSE, -1);  // release the helper
+        lds_flag_put(rp.fl + F_BLKUSE, -1);  // this pipe needs no more blocks
         wake_helper();
         if (B.mt_state_out) {
             uint32_t *o = B.mt_state_out + (size_t)s * 625;
@@ -846,13 +877,37 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
         }
 #endif
     } else {
-        // ---- helper: twists on demand, asleep otherwise
+        // ---- helper: twists on demand for every parser of the workgroup, asleep otherwise
+        __syncthreads();
         __builtin_amdgcn_s_setprio(3);
 #ifdef LSLAM_STAMPS
         if (a.dbg && lane == 0)
-            a.dbg[(size_t)s * 16 + 12] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+            for (int j = 0; j < PPW; j++)
+                if ((int)blockIdx.x * PPW + j < B.n_scans)
+                    a.dbg[((size_t)blockIdx.x * PPW + j) * 16 + 12] =
+                        (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
 #endif
-        rng_helper(rp, lane);
+        int produced[PPW];
+#pragma unroll
+        for (int j = 0; j < PPW; j++) produced[j] = 0;
+        for (;;) {
+            bool busy = false, live = false;
+#pragma unroll
+            for (int j = 0; j < PPW; j++) {
+                RngPipe rp = pipe_of(j);
+                const int use = lds_flag_get(rp.fl + F_BLKUSE);
+                if (use < 0) continue;  // parser finished
+                live = true;
+                if (use == produced[j]) {
+                    mt_twist_oop(rp.blk + (produced[j] & 1) * MT_N, rp.blk + ((produced[j] + 1) & 1) * MT_N, lane);
+                    produced[j] += 1;
+                    lds_flag_put(rp.fl + F_BLK, produced[j]);
+                    busy = true;
+                }
+            }
+            if (!live) break;
+            if (!busy) __builtin_amdgcn_s_sleep(127);  // until a parser's s_wakeup
+        }
     }
 }
 
@@ -863,24 +918,24 @@ __global__ __launch_bounds__(128) void rng_kernel(const KArgs a) {
 template <typename JT>
 __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int c = blockIdx.x;
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
-    const int p0 = B.chunk_pt_off[c];
-    const int N = B.chunk_pt_off[c + 1] - p0;
-    if (N < 3) return;
     const uint32_t D = (uint32_t)a.T + 1u;
-    resolve_chunk((const JT *)a.jbuf + (size_t)D * (size_t)p0, (uint32_t)N - 1u, D, (uint32_t)a.res_g, smem,
-                  a.draws_scr + (size_t)c * 2 * D, lane);
+    for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N >= 3)
+            resolve_chunk((const JT *)a.jbuf + (size_t)D * (size_t)p0, (uint32_t)N - 1u, D, (uint32_t)a.res_g, smem,
+                          a.draws_scr + (size_t)c * 2 * D, lane);
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------
 // chunk_kernel: one wave per chunk, A4-A8 with the draws given
 // ------------------------------------------------------------------------
 template <int HYP>
-__global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int c = blockIdx.x;
+__device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned char *smem) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
     double2 *P = (double2 *)(smem + a.off_pts);
@@ -943,6 +998,15 @@ __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
         for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
     }
     if (lane == 0 && B.models) B.models[c] = rec;
+}
+
+template <int HYP>
+__global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    for (int c = blockIdx.x; c < a.b.n_chunks; c += gridDim.x) {
+        chunk_body<HYP>(a, c, smem);
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1015,31 +1079,6 @@ __device__ __forceinline__ void trial_pair(const KArgs &a, int c, int N, int D, 
         i0 = h[0];
         i1 = h[1];
     }
-}
-
-// largest x >= 0 with fl(x*x) < e (-1 if none), smallest x with fl(x*x) > e
-__device__ __forceinline__ double sq_floor_lt(double e) {
-    if (!(e > 0.0)) return -1.0;
-    double x = sqrt(e);
-    while (x > 0.0 && x * x >= e) x = __longlong_as_double(__double_as_longlong(x) - 1);
-    for (;;) {
-        const double y = __longlong_as_double(__double_as_longlong(x) + 1);
-        if (y * y < e) x = y;
-        else break;
-    }
-    return x;
-}
-__device__ __forceinline__ double sq_ceil_gt(double e) {
-    if (!(e >= 0.0)) return 0.0;
-    double x = sqrt(e);
-    while (x * x <= e) x = __longlong_as_double(__double_as_longlong(x) + 1);
-    for (;;) {
-        if (x == 0.0) break;
-        const double y = __longlong_as_double(__double_as_longlong(x) - 1);
-        if (y * y > e) x = y;
-        else break;
-    }
-    return x;
 }
 
 // A4 for every trial of every large chunk (and the Philox draws they use)
@@ -1435,6 +1474,10 @@ struct lslam_ctx {
     // large-chunk consensus scratch: per-trial counts (+ Philox draws)
     void *cscr;
     size_t cscr_bytes;
+    // grid cap of the one-wave consumer kernels (resolve, chunk, fix-up, post)
+    int consumer_wgs;
+    // parser waves per producer workgroup (one helper each)
+    int rng_ppw;
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
@@ -1512,6 +1555,13 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->escr_bytes = 0;
     c->cscr = nullptr;
     c->cscr_bytes = 0;
+    c->consumer_wgs = 1 << 30;
+    c->rng_ppw = 4;
+    if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
+    if (const char *e = getenv("LSLAM_CONSUMER_WGS")) {
+        const int v = atoi(e);
+        if (v > 0) c->consumer_wgs = v;
+    }
     c->pstream = nullptr;
     c->pslot[0] = c->pslot[1] = nullptr;
     c->pslot_bytes = 0;
@@ -1534,7 +1584,14 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
             HIPCHK(hipEventCreate(&c->ev0[k][r]));
             HIPCHK(hipEventCreate(&c->ev1[k][r]));
         }
-    HIPCHK(hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    // the producer's chains are the critical path: its stream gets the highest
+    // priority so that its workgroups are dispatched ahead of the previous call's
+    // consumers (resolve / consensus / post) that run beside it
+    {
+        int lo_pri = 0, hi_pri = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
+        HIPCHK(hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, hi_pri));
+    }
     HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[1], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
@@ -1926,14 +1983,19 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
 }
 
 // rng_kernel LDS: two raw MT blocks + flags
-static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
+static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
     const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
     int off = 0;
     k.off_blk = off; off += align16(2 * 4 * 624);
     k.off_fl = off; off += align16(4 * F_NFLAGS);
-    lds = off;
+    k.rng_pipe_bytes = off;
+    lds = off * ppw;
     return LSLAM_OK;
+}
+
+static inline unsigned launch_cap(const lslam_ctx *c, int64_t n) {
+    return (unsigned)(n < c->consumer_wgs ? (n > 0 ? n : 1) : c->consumer_wgs);
 }
 
 static int ensure_scratch(lslam_ctx *c, size_t bytes) {
@@ -2013,7 +2075,7 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         set_max_lds(resolve_kernel<uint8_t>);
         set_max_lds(resolve_kernel<uint16_t>);
     });
-    const dim3 grid((unsigned)k.b.n_chunks), block(64);
+    const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
     if (k.j8) hipLaunchKernelGGL(resolve_kernel<uint8_t>, grid, block, lds, c->stream, k);
     else hipLaunchKernelGGL(resolve_kernel<uint16_t>, grid, block, lds, c->stream, k);
     HIPCHK(hipGetLastError());
@@ -2023,17 +2085,26 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
 static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
     int lds = 0;
-    int st = layout_rng(k, &k.b, lds);
+    const int ppw = c->rng_ppw;
+    int st = layout_rng(k, &k.b, lds, ppw);
     if (st) return st;
     static std::once_flag once;
     std::call_once(once, [] {
-        set_max_lds(rng_kernel<uint8_t>);
-        set_max_lds(rng_kernel<uint16_t>);
+        set_max_lds(rng_kernel<uint8_t, 1>);
+        set_max_lds(rng_kernel<uint16_t, 1>);
+        set_max_lds(rng_kernel<uint8_t, 4>);
+        set_max_lds(rng_kernel<uint16_t, 4>);
     });
     st = timer_begin(c, LSLAM_K_RNG, stream);
     if (st) return st;
-    if (k.j8) hipLaunchKernelGGL(rng_kernel<uint8_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, stream, k);
-    else hipLaunchKernelGGL(rng_kernel<uint16_t>, dim3((unsigned)k.b.n_scans), dim3(128), lds, stream, k);
+    const dim3 grid((unsigned)((k.b.n_scans + ppw - 1) / ppw)), block(64 * (ppw + 1));
+    if (ppw == 4) {
+        if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t, 4>), grid, block, lds, stream, k);
+        else hipLaunchKernelGGL((rng_kernel<uint16_t, 4>), grid, block, lds, stream, k);
+    } else {
+        if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t, 1>), grid, block, lds, stream, k);
+        else hipLaunchKernelGGL((rng_kernel<uint16_t, 1>), grid, block, lds, stream, k);
+    }
     HIPCHK(hipGetLastError());
     return timer_end(c, LSLAM_K_RNG, stream);
 }
@@ -2177,7 +2248,7 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
         set_max_lds(chunk_kernel<LSLAM_HYP_PHILOX>);
         set_max_lds(chunk_kernel<LSLAM_HYP_EXPLICIT>);
     });
-    const dim3 grid((unsigned)k.b.n_chunks), block(64);
+    const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
     switch (k.hyp_source) {
         case LSLAM_HYP_PHILOX: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_PHILOX>, grid, block, lds, c->stream, k); break;
         case LSLAM_HYP_EXPLICIT: hipLaunchKernelGGL(chunk_kernel<LSLAM_HYP_EXPLICIT>, grid, block, lds, c->stream, k); break;
@@ -2191,7 +2262,8 @@ template <int MODE>
 static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
     static std::once_flag once;
     std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>); });
-    hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), dim3((unsigned)k.b.n_scans), dim3(64), lds, c->stream, k);
+    hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), dim3(launch_cap(c, k.b.n_scans)), dim3(64), lds, c->stream,
+                       k);
     HIPCHK(hipGetLastError());
     return LSLAM_OK;
 }
@@ -2244,7 +2316,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         kf.fixup = 1;
         static std::once_flag once;
         std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>); });
-        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3((unsigned)b->n_scans), dim3(64), lds_fix,
+        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_fix,
                            c->stream, kf);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));

@@ -127,6 +127,31 @@ __device__ __forceinline__ double pw_sum(const double2 *P, int n, const Model &m
     return vstack[lane];
 }
 
+// largest x >= 0 with fl(x*x) < e (-1 if none), smallest x with fl(x*x) > e
+__device__ __forceinline__ double sq_floor_lt(double e) {
+    if (!(e > 0.0)) return -1.0;
+    double x = sqrt(e);
+    while (x > 0.0 && x * x >= e) x = __longlong_as_double(__double_as_longlong(x) - 1);
+    for (;;) {
+        const double y = __longlong_as_double(__double_as_longlong(x) + 1);
+        if (y * y < e) x = y;
+        else break;
+    }
+    return x;
+}
+__device__ __forceinline__ double sq_ceil_gt(double e) {
+    if (!(e >= 0.0)) return 0.0;
+    double x = sqrt(e);
+    while (x * x <= e) x = __longlong_as_double(__double_as_longlong(x) + 1);
+    for (;;) {
+        if (x == 0.0) break;
+        const double y = __longlong_as_double(__double_as_longlong(x) - 1);
+        if (y * y > e) x = y;
+        else break;
+    }
+    return x;
+}
+
 // closed-form principal direction of the centred inliers (replaces dgesdd's
 // v[0], fit.py:94); identical formula in oracle/ransac_oracle.c
 __device__ __forceinline__ void tls_direction(double sxx, double sxy, double syy, double &ux, double &uy) {
