@@ -213,6 +213,10 @@ enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMAR
        LSLAM_K_EXPRESS = 7 /* a whole express decode / scans call */,
        LSLAM_K_EXPRESS_SCATTER = 8 /* its decode + A1 + scatter kernel */, LSLAM_K_COUNT = 9 };
 int lslam_set_timing(lslam_ctx *ctx, int enable);
+/* which kernel ids are timed while timing is on (bit k = LSLAM_K_k; default all).  Timing
+ * events between the producer and consumer kernels change how the two streams overlap,
+ * so a throughput measurement should time only the kernel it reports. */
+int lslam_set_timing_mask(lslam_ctx *ctx, uint32_t mask);
 int lslam_timing(lslam_ctx *ctx, int kernel, double *total_ms, int64_t *launches);  /* syncs */
 int lslam_timing_reset(lslam_ctx *ctx);
 

@@ -86,7 +86,8 @@ assert C.sizeof(LandmarkRec) == 56
 EXPORTS = [
     "lslam_version", "lslam_status_string", "lslam_last_error", "lslam_device_count", "lslam_ctx_create",
     "lslam_ctx_destroy", "lslam_sync", "lslam_malloc", "lslam_free", "lslam_host_alloc", "lslam_host_free",
-    "lslam_h2d", "lslam_d2h", "lslam_memset", "lslam_set_timing", "lslam_timing", "lslam_timing_reset",
+    "lslam_h2d", "lslam_d2h", "lslam_memset", "lslam_set_timing", "lslam_set_timing_mask", "lslam_timing",
+    "lslam_timing_reset",
     "lslam_ransac_params_default", "lslam_ukf_params_default", "lslam_inlier_cutoff", "lslam_ukf_weights",
     "lslam_mt_seed_state", "lslam_polar_to_xy", "lslam_hyp_mt19937", "lslam_ransac", "lslam_landmarks",
     "lslam_ukf_step", "lslam_scan_pipeline", "lslam_express_decode", "lslam_express_scans",
@@ -130,6 +131,7 @@ def load():
         "lslam_d2h": ([_VP, _VP, _VP, sz], C.c_int),
         "lslam_memset": ([_VP, _VP, C.c_int, sz], C.c_int),
         "lslam_set_timing": ([_VP, C.c_int], C.c_int),
+        "lslam_set_timing_mask": ([_VP, u32], C.c_int),
         "lslam_timing": ([_VP, C.c_int, P(dbl), P(i64)], C.c_int),
         "lslam_timing_reset": ([_VP], C.c_int),
         "lslam_ransac_params_default": ([P(RansacParams)], C.c_int),

@@ -841,8 +841,8 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
             const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
             if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
         }
-        rp.prio = 2;
-        set_prio_level(2);
+        rp.prio = RP_PRIO_TOP;
+        set_prio_level(RP_PRIO_TOP);
         int blkno = 0;
         int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
         JT *J = (JT *)a.jbuf;
@@ -1476,6 +1476,7 @@ struct lslam_ctx {
     size_t cscr_bytes;
     // grid cap of the one-wave consumer kernels (resolve, chunk, fix-up, post)
     int consumer_wgs;
+    uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
     int rng_ppw;
     // The MT producer of call k+1 runs on its own stream while call k's
@@ -1556,6 +1557,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->cscr = nullptr;
     c->cscr_bytes = 0;
     c->consumer_wgs = 1 << 30;
+    c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
     if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
     if (const char *e = getenv("LSLAM_CONSUMER_WGS")) {
@@ -1708,7 +1710,7 @@ static int harvest(lslam_ctx *c, int k, int upto_free = -1) {
 }
 
 static int timer_begin(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
-    if (!c->timing) return LSLAM_OK;
+    if (!c->timing || !((c->timing_mask >> k) & 1u)) return LSLAM_OK;
     int st = harvest(c, k, 1);
     if (st) return st;
     HIPCHK(hipEventRecord(c->ev0[k][c->head[k]], st_ ? st_ : c->stream));
@@ -1716,7 +1718,7 @@ static int timer_begin(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
 }
 
 static int timer_end(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
-    if (!c->timing) return LSLAM_OK;
+    if (!c->timing || !((c->timing_mask >> k) & 1u)) return LSLAM_OK;
     HIPCHK(hipEventRecord(c->ev1[k][c->head[k]], st_ ? st_ : c->stream));
     c->head[k] = (c->head[k] + 1) % LSLAM_EV_RING;
     c->npend[k] += 1;
@@ -1726,6 +1728,12 @@ static int timer_end(lslam_ctx *c, int k, hipStream_t st_ = nullptr) {
 int lslam_set_timing(lslam_ctx *c, int en) {
     if (!c) return LSLAM_ERR_ARG;
     c->timing = en != 0;
+    return LSLAM_OK;
+}
+
+int lslam_set_timing_mask(lslam_ctx *c, uint32_t mask) {
+    if (!c) return LSLAM_ERR_ARG;
+    c->timing_mask = mask;
     return LSLAM_OK;
 }
 

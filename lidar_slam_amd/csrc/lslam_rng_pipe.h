@@ -47,8 +47,14 @@ __device__ __forceinline__ void wake_helper() { asm volatile("s_wakeup" ::: "mem
 
 // Waves of a SIMD issue by priority, then age.  With equal priorities the
 // oldest parser of a SIMD races ahead and the youngest finishes last.
-// Parsers lower their priority as they progress (2 in the first third of the
-// scan's steps ... 0 in the last) so the SIMD's parsers advance together.
+// Parsers lower their priority as they progress (RP_PRIO_TOP in the first
+// third of the scan's steps ... RP_PRIO_TOP - 2 in the last) so the SIMD's
+// parsers advance together.  The bottom level stays above 0, the priority of
+// the consumer kernels (resolve / consensus / post of the previous call) that
+// share the SIMDs: they take the issue slots the parsers' chains leave idle.
+#ifndef RP_PRIO_TOP
+#define RP_PRIO_TOP 3
+#endif
 __device__ __forceinline__ void set_prio_level(int lvl) {
     switch (lvl) {
         case 3: __builtin_amdgcn_s_setprio(3); break;
@@ -145,7 +151,7 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             pre_pos = -1;
             lds_flag_put(rp.fl + F_BLKUSE, blkno);
             wake_helper();
-            const int lvl = 2 - (int)(((uint64_t)(rp.done_steps + g) * 3u) / (rp.total_steps + 1u));
+            const int lvl = RP_PRIO_TOP - (int)(((uint64_t)(rp.done_steps + g) * 3u) / (rp.total_steps + 1u));
             if (lvl != rp.prio) {
                 rp.prio = lvl;
                 set_prio_level(lvl);

@@ -31,7 +31,10 @@ class Context:
     def sync(self):
         _lib.check(self._L.lslam_sync(self.handle), "lslam_sync")
 
-    def set_timing(self, on: bool = True):
+    def set_timing(self, on: bool = True, kernels=None):
+        """HIP-event timing of the kernel ids in ``kernels`` (default: all)."""
+        mask = 0xFFFFFFFF if kernels is None else sum(1 << int(k) for k in kernels)
+        _lib.check(self._L.lslam_set_timing_mask(self.handle, mask), "lslam_set_timing_mask")
         _lib.check(self._L.lslam_set_timing(self.handle, 1 if on else 0), "lslam_set_timing")
 
     def timing(self, kernel: int):
