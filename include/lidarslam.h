@@ -75,7 +75,20 @@ enum {
 enum {
     LSLAM_UKF_PREDICT = 1,
     LSLAM_UKF_UPDATE = 2,
-    LSLAM_UKF_LMK_FROM_RANSAC = 4  /* landmark slot c <- chunk c's Landmark.pos (fused pipeline) */
+    LSLAM_UKF_LMK_FROM_RANSAC = 4, /* landmark slot c <- chunk c's Landmark.pos (fused pipeline) */
+    /* Landmark MAP mode (lslam_scan_pipeline with landmarks only): each scan's
+     * landmark list is a persistent WORLD-frame map.  Per scan: predict (if PREDICT); every fitted
+     * chunk line (ransac_functions.py:25-31, robot frame) is moved into the world frame by the
+     * predicted pose x = [tx, ty, th] (p_w = R(th) p + t; a, b from the rotated direction); the
+     * association walk (ransac_functions.py:34-54) runs on the map; each chunk that MATCHED a map
+     * landmark j becomes one range/bearing measurement against hx(x, pos_j) (UKFMethods.py:26-34):
+     * z_c = [|f|, atan2(f_y, f_x)], f = the foot of pos_j (moved into the robot frame by the
+     * predicted pose) on the chunk's fitted line (is_equal matches any segment continuing the same
+     * wall, so the chunk's own origin is not pos_j's re-observation); update (if UPDATE and >= 1
+     * match) with those measurements only.  ukf_z / ukf_lmk are not read; n_landmarks = measurement slots, one per
+     * chunk of a scan (>= max_scan_chunks); R_diag[2c], R_diag[2c+1] is slot c's noise.
+     * models[c] keeps the robot-frame fit; proj_a/proj_b (y_proj) stay the chunk's own line. */
+    LSLAM_UKF_MAP = 8
 };
 
 /* One RANSAC call's result (one chunk), 112 bytes. */
@@ -160,8 +173,8 @@ typedef struct lslam_scan_batch {
     double *ukf_x;                  /* [n_scans][3] in/out */
     double *ukf_P;                  /* [n_scans][3][3] in/out */
     const double *ukf_u;            /* [n_scans][2]  [vl, vr] */
-    const double *ukf_z;            /* [n_scans][2L] interleaved [d0, phi0, d1, phi1, ...] */
-    const double *ukf_lmk;          /* [n_scans][L][2] landmark positions */
+    const double *ukf_z;            /* [n_scans][2L] interleaved [d0, phi0, d1, phi1, ...] (not in MAP mode) */
+    const double *ukf_lmk;          /* [n_scans][L][2] landmark positions (not in MAP mode) */
     const double *ukf_R_diag;       /* [2L] measurement noise diagonal (systemClass.py:28) */
 } lslam_scan_batch;
 

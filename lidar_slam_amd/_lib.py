@@ -25,7 +25,7 @@ EARLY_STOP, VERTICAL, NEW_LANDMARK, MATCHED = 16, 32, 64, 128
 CAPACITY = 256
 
 HYP_MT19937, HYP_PHILOX, HYP_EXPLICIT = 0, 1, 2
-UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC = 1, 2, 4
+UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC, UKF_MAP = 1, 2, 4, 8
 K_POLAR, K_HYP, K_PIPELINE, K_LANDMARK, K_UKF, K_RNG, K_CONSENSUS = 0, 1, 2, 3, 4, 5, 6
 K_EXPRESS, K_EXPRESS_SCATTER = 7, 8
 

@@ -58,7 +58,7 @@ struct KArgs {
     int life;
     // LDS layout (byte offsets into dynamic shared memory)
     int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum, off_inl;
-    int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg;
+    int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg, off_zobs;
     int corg_cap;
     int off_ukf;
     int off_j1;
@@ -465,7 +465,7 @@ __device__ __forceinline__ bool is_equal(const lslam_landmark &Lk, double a, dou
 // returns match index (pre-call) or -1; updates list + count; proj line out
 __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, int &L, double a, double b,
                          double px, double py, double ex, double ey, int id, double &pa, double &pb,
-                         bool &overflow, int32_t *walk_out, int lane) {
+                         bool &overflow, int32_t *walk_out, int lane, double2 *mpos = nullptr) {
     const int nblk = (L + 63) >> 6;
     for (int i = lane; i < nblk; i += 64) vis[i] = 0ull;
     __syncthreads();
@@ -503,6 +503,7 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
     if (match >= 0) {
         pa = unid(lmk[match].a);
         pb = unid(lmk[match].b);
+        if (mpos) *mpos = make_double2(unid(lmk[match].pos_x), unid(lmk[match].pos_y));
     }
     // apply decrease_life / removal / reset_life, then compact in list order
     int w = 0;
@@ -548,6 +549,46 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
 }
 
 // ------------------------------------------------------------------------
+// landmark map (LSLAM_UKF_MAP): a fitted chunk line (robot frame,
+// ransac_functions.py:25-31) moved into the world frame of pose (tx, ty, th):
+// p_w = R(th) p + t for the origin and the tip, the direction rotated, then
+// a, b exactly as ransac_functions.py:26-27 form them.  At th = 0, t = 0 every
+// value is unchanged bit for bit (c = 1, s = 0).
+// ------------------------------------------------------------------------
+struct MapLine {
+    double a, b, px, py, ex, ey;
+};
+__device__ __forceinline__ MapLine to_world(const lslam_chunk_model &r, double c, double s, double tx, double ty) {
+    MapLine w;
+    w.px = (c * r.ox - s * r.oy) + tx;
+    w.py = (s * r.ox + c * r.oy) + ty;
+    w.ex = (c * r.tip_x - s * r.tip_y) + tx;
+    w.ey = (s * r.tip_x + c * r.tip_y) + ty;
+    const double ux = c * r.ux - s * r.uy;
+    const double uy = s * r.ux + c * r.uy;
+    w.a = uy / ux;
+    w.b = w.py - w.a * w.px;
+    return w;
+}
+
+// The measurement a chunk that matched map landmark j contributes (robot frame):
+// is_equal (landmarking.py:66-77) matches any segment continuing the same wall,
+// so the chunk's own origin may lie a segment length away from pos_j.  The
+// measured point is instead the foot of pos_j (moved into the robot frame by the
+// predicted pose) on the observed line o + t u; z = [|f|, atan2(f_y, f_x)] is
+// compared with hx(x, pos_j) (UKFMethods.py:26-34).  Same wall => consistent.
+__device__ __forceinline__ double2 observe_point(const lslam_chunk_model &r, double2 pw, double c, double s, double tx,
+                                                 double ty) {
+    const double dx = pw.x - tx, dy = pw.y - ty;
+    const double qx = c * dx + s * dy;
+    const double qy = c * dy - s * dx;
+    const double t = (qx - r.ox) * r.ux + (qy - r.oy) * r.uy;
+    const double fx = r.ox + t * r.ux;
+    const double fy = r.oy + t * r.uy;
+    return make_double2(cr_sqrt(fx * fx + fy * fy), atan2(fy, fx));
+}
+
+// ------------------------------------------------------------------------
 // the scan kernel
 // ------------------------------------------------------------------------
 template <int HYP, int MODE>
@@ -567,6 +608,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
     int *nstack = (int *)(smem + a.off_nstack);
     int32_t *hist = (int32_t *)(smem + a.off_hist);
     double2 *corg = (double2 *)(smem + a.off_corg);
+    double2 *zobs = (double2 *)(smem + a.off_zobs);
     lslam_landmark *lmk = (lslam_landmark *)(smem + a.off_lmk);
     uint64_t *vis = (uint64_t *)(smem + a.off_vis);
 
@@ -626,6 +668,28 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         __syncthreads();
     }
     const int id0 = B.id_base ? B.id_base[s] : 0;
+
+    // landmark MAP mode (LSLAM_UKF_MAP): predict first; the chunks' lines are
+    // associated in the world frame of the predicted pose; matches feed the update
+    constexpr bool kMapable = kPost && (MODE & MODE_ASSOC) && (MODE & MODE_UKF);
+    const bool map_mode = kMapable && (a.ukf.flags & LSLAM_UKF_MAP);
+    double mx[3], mP[9], mu[2];
+    double cth = 1.0, sth = 0.0;
+    int n_meas = 0;
+    if (kMapable && map_mode) {
+        for (int i = 0; i < 3; i++) mx[i] = B.ukf_x[3 * (size_t)s + i];
+        for (int i = 0; i < 9; i++) mP[i] = B.ukf_P[9 * (size_t)s + i];
+        mu[0] = B.ukf_u[2 * (size_t)s];
+        mu[1] = B.ukf_u[2 * (size_t)s + 1];
+        if (a.ukf.flags & LSLAM_UKF_PREDICT) {
+            UkfLds us;
+            us.carve((double *)(smem + a.off_ukf), a.ukf.L);
+            ukf_step(mx, mP, mu[0], mu[1], nullptr, B.ukf_R_diag,
+                     [](int, double &, double &) { return false; }, a.ukf, LSLAM_UKF_PREDICT, us, lane);
+        }
+        cth = cos(mx[2]);
+        sth = sin(mx[2]);
+    }
 
     for (int ci = 0; ci < nchunks && (kRansac || kPost); ci++) {
         const int c = c0 + ci;
@@ -708,7 +772,31 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 
         // ---- A9/A10 association + projection
         if (MODE & MODE_ASSOC) {
-            if (have_model) {
+            if (kMapable && map_mode) {
+                if (ci < a.corg_cap && lane == 0) corg[ci] = make_double2(__builtin_nan(""), __builtin_nan(""));
+            }
+            if (kMapable && map_mode && have_model) {
+                // the chunk's line in the world frame of the predicted pose
+                const MapLine w = to_world(rec, cth, sth, mx[0], mx[1]);
+                double pa, pb;
+                bool overflow = false;
+                double2 mp = make_double2(0.0, 0.0);
+                const int m = associate(a, lmk, vis, L, w.a, w.b, w.px, w.py, w.ex, w.ey, rec.landmark_id, pa, pb,
+                                        overflow, B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr, lane,
+                                        &mp);
+                rec.match_index = m;
+                rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
+                if (overflow) rec.flags |= LSLAM_CAPACITY;
+                if (m >= 0 && ci < a.corg_cap) {
+                    // measurement of map landmark m (hx = range/bearing of its pos): the point of the
+                    // observed line nearest to that pos seen from the predicted pose (observe_point)
+                    if (lane == 0) {
+                        corg[ci] = mp;
+                        zobs[ci] = observe_point(rec, mp, cth, sth, mx[0], mx[1]);
+                    }
+                    n_meas++;
+                }
+            } else if (have_model) {
                 double pa, pb;
                 bool overflow = false;
                 const int m = associate(a, lmk, vis, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
@@ -747,8 +835,30 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         if (lane == 0) B.lmk_count[s] = L;
     }
 
+    // ---- UKF update of MAP mode: the matched chunks are the measurements
+    if (kMapable && map_mode) {
+        __syncthreads();
+        if ((a.ukf.flags & LSLAM_UKF_UPDATE) && n_meas > 0) {
+            const int nslot = min(nchunks, a.corg_cap);
+            auto slot_fn = [&](int j, double &px, double &py) {
+                if (j >= nslot) return false;
+                const double2 q = corg[j];
+                px = q.x;
+                py = q.y;
+                return q.x == q.x;
+            };
+            UkfLds us;
+            us.carve((double *)(smem + a.off_ukf), a.ukf.L);
+            ukf_step(mx, mP, mu[0], mu[1], (const double *)zobs, B.ukf_R_diag, slot_fn, a.ukf, LSLAM_UKF_UPDATE, us,
+                     lane);
+        }
+        if (lane == 0) {
+            for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = mx[i];
+            for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = mP[i];
+        }
+    }
     // ---- UKF step (U1-U8)
-    if (MODE & MODE_UKF) {
+    if ((MODE & MODE_UKF) && !map_mode) {
         __syncthreads();
         double x[3], Pm[9], u[2];
         for (int i = 0; i < 3; i++) x[i] = B.ukf_x[3 * (size_t)s + i];
@@ -766,10 +876,11 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 const double2 q = corg[j];
                 if (q.x == q.x) { px = q.x; py = q.y; }
             }
+            return true;
         };
         UkfLds us;
         us.carve((double *)(smem + a.off_ukf), Lu);
-        ukf_step(x, Pm, u[0], u[1], B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, us, lane);
+        ukf_step(x, Pm, u[0], u[1], B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, a.ukf.flags, us, lane);
         if (lane == 0) {
             for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = x[i];
             for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
@@ -1906,6 +2017,7 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     k.off_hist = off; off += align16(4 * k.hist_cap);
     k.corg_cap = k.hist_cap;
     k.off_corg = off; off += align16(16 * k.corg_cap);
+    k.off_zobs = off; off += (u && (u->flags & LSLAM_UKF_MAP)) ? align16(16 * k.corg_cap) : 0;
     k.lmk_cap = (mode & MODE_ASSOC) ? b->lmk_capacity : 0;
     if ((mode & MODE_ASSOC) && k.lmk_cap <= 0) return set_err(LSLAM_ERR_ARG, "lmk_capacity must be > 0");
     k.off_lmk = off; off += align16((int)sizeof(lslam_landmark) * (k.lmk_cap > 0 ? k.lmk_cap : 1));
@@ -1913,8 +2025,13 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     k.pts_cap = N;
     if (u) {
         if (u->n_landmarks <= 0) return set_err(LSLAM_ERR_ARG, "n_landmarks must be > 0");
-        if (!b->ukf_x || !b->ukf_P || !b->ukf_u || !b->ukf_z || !b->ukf_lmk || !b->ukf_R_diag)
+        const bool map = (u->flags & LSLAM_UKF_MAP) != 0;
+        if (!b->ukf_x || !b->ukf_P || !b->ukf_u || !b->ukf_R_diag || (!map && (!b->ukf_z || !b->ukf_lmk)))
             return set_err(LSLAM_ERR_ARG, "UKF buffers missing");
+        if (map && (!(mode & MODE_ASSOC) || !b->landmarks))
+            return set_err(LSLAM_ERR_ARG, "LSLAM_UKF_MAP needs the landmark lists (the map) in lslam_scan_pipeline");
+        if (map && u->n_landmarks < b->max_scan_chunks)
+            return set_err(LSLAM_ERR_CAPACITY, "LSLAM_UKF_MAP: n_landmarks (measurement slots) < max_scan_chunks");
         double lpn = 0;
         lslam_ukf_weights(u, k.ukf.Wm, k.ukf.Wc, &lpn);
         for (int i = 0; i < 7; i++)

@@ -103,14 +103,18 @@ __device__ __forceinline__ void fx(const double s[3], double dt, double u0, doub
     o[2] = s[2] + dt * b2;
 }
 
-// One UKF step for one scan; x[3], P[9] in/out (uniform).  Returns false if a
-// factorisation failed (non-SPD P or singular M).
+// One UKF step for one scan; x[3], P[9] in/out (uniform).  `flags` = the
+// predict (1) / update (2) bits to run.  lmk(j, px, py) gives landmark j's
+// position and returns whether measurement slot j is active: an inactive slot's
+// rows of Y and y are zero, so it adds exactly nothing to G = Y R^-1 Y^T and
+// b = Y R^-1 y (the update equals one over the active measurements alone).
+// Returns false if a factorisation failed (non-SPD P or singular M).
 template <typename LmkFn>
 __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const double *z, const double *Rd,
-                         LmkFn lmk, const UkfConst &C, UkfLds &S, int lane) {
+                         LmkFn lmk, const UkfConst &C, int flags, UkfLds &S, int lane) {
     bool ok = true;
     double U[9];
-    if (C.flags & 1) {  // ---- predict (filterpy UKF.predict)
+    if (flags & 1) {  // ---- predict (filterpy UKF.predict)
         {
             double A[9];
             for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
@@ -151,7 +155,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         x[2] = xm2;
         __syncthreads();
     }
-    if (!(C.flags & 2)) return ok;
+    if (!(flags & 2)) return ok;
     // ---- sigmas_f re-drawn from (x, P) (end of predict; also the update-only case)
     {
         double A[9];
@@ -176,7 +180,15 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         const int j = j0 + lane;
         if (j < C.L) {
             double px, py;
-            lmk(j, px, py);
+            if (!lmk(j, px, py)) {
+                for (int k = 0; k < 7; k++) {
+                    S.Y[k * m2 + 2 * j] = 0.0;
+                    S.Y[k * m2 + 2 * j + 1] = 0.0;
+                }
+                S.yr[2 * j] = 0.0;
+                S.yr[2 * j + 1] = 0.0;
+                continue;
+            }
             double d[7], ph[7];
             for (int k = 0; k < 7; k++) {
                 const double dx = px - S.sig[3 * k], dy = py - S.sig[3 * k + 1];

@@ -57,6 +57,57 @@ def scan_polar(scan_id: int, n_beams: int = 720, cfg: int = 0, dropout: float = 
     return theta, dist, np.array([px, py, heading])
 
 
+def scan_polar_at(pose, scan_id: int, n_beams: int = 720, cfg: int = 0):
+    """(theta_deg, dist_mm) of one revolution seen from a GIVEN pose (x, y,
+    heading): the landmark-map trajectories (``trajectory``).  Same beam model
+    and noise as ``scan_polar``, its own seed stream."""
+    rng = np.random.default_rng(1_000_003 * int(scan_id) + int(cfg) + 0x5A17)
+    px, py, heading = (float(v) for v in pose)
+    theta = np.arange(n_beams, dtype=np.float64) * (360.0 / n_beams)
+    world = heading + (np.pi / 2 - np.deg2rad(theta))
+    dist = _ray_room(px, py, world) + rng.normal(0.0, NOISE_MM, n_beams)
+    out = rng.random(n_beams) < OUTLIER_FRAC
+    dist = np.where(out, rng.uniform(150.0, 5000.0, n_beams), dist)
+    return theta, dist
+
+
+def trajectory(robot_ids, n_steps: int, u=(2.0, 2.5), dt: float = 0.005, wheel_radius: float = 50.0,
+               wheel_base: float = 200.0):
+    """True poses [n_steps + 1, R, 3] of R robots driven by wheel speeds u with
+    the motion model of UKFMethods.py:17-24 (intended form); start poses as
+    ``scan_polar``'s (uniform in the room, 800 mm margin, heading on (-pi, pi])."""
+    R = len(robot_ids)
+    poses = np.zeros((n_steps + 1, R, 3))
+    for i, r in enumerate(robot_ids):
+        rng = np.random.default_rng(1_000_003 * int(r) + 77)
+        poses[0, i] = (rng.uniform(MARGIN, ROOM_W - MARGIN), rng.uniform(MARGIN, ROOM_H - MARGIN),
+                       -rng.uniform(-np.pi, np.pi))
+    vl, vr = u
+    for k in range(n_steps):
+        th = poses[k, :, 2]
+        v = wheel_radius / 2.0 * (vl + vr)
+        poses[k + 1, :, 0] = poses[k, :, 0] + dt * v * np.cos(th)
+        poses[k + 1, :, 1] = poses[k, :, 1] + dt * v * np.sin(th)
+        poses[k + 1, :, 2] = th + dt * (wheel_radius / wheel_base) * (vr - vl)
+    return poses
+
+
+def revolutions_at(poses, step: int, robot_ids, n_beams: int = 720):
+    """One revolution per robot from its true pose at ``step`` (``trajectory``),
+    in the chunked CSR layout of ``make_batch`` (robot r = scan r)."""
+    xs, sco, cpo = [], [0], [0]
+    sizes = chunk_sizes(n_beams)
+    used = int(sum(sizes))
+    for i, r in enumerate(robot_ids):
+        th, d = scan_polar_at(poses[i], 1_000 * int(r) + int(step), n_beams)
+        xs.append(polar_to_xy_ref(th, d)[:used])
+        for n in sizes:
+            cpo.append(cpo[-1] + n)
+        sco.append(sco[-1] + len(sizes))
+    return {"xy": np.ascontiguousarray(np.concatenate(xs, axis=0)),
+            "scan_chunk_off": np.asarray(sco, dtype=np.int32), "chunk_pt_off": np.asarray(cpo, dtype=np.int32)}
+
+
 def polar_to_xy_ref(theta_deg, dist):
     """NumPy form of ``functions.py:59-60`` (x = d*cos(-theta*A + pi/2))."""
     a = -np.asarray(theta_deg, dtype=np.float64) * (np.pi / 180) + np.pi / 2

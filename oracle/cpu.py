@@ -56,6 +56,10 @@ def lib():
                                              P(C.c_uint32), P(C.c_int32), P(Landmark), P(C.c_int32),
                                              C.c_int32, P(C.c_uint8), P(C.c_double), P(ChunkModel)]
         L.or_is_equal.argtypes = [P(Landmark), P(Landmark)]
+        L.or_associate.argtypes = [P(Landmark), P(C.c_int32), C.c_int32, P(Landmark), P(C.c_int32),
+                                   P(C.c_double), P(C.c_double)]
+        L.or_associate.restype = C.c_int32
+        L.or_set_tolerances.argtypes = [C.c_double, C.c_double, C.c_double]
         _lib = L
     return _lib
 
@@ -165,6 +169,25 @@ def landmark_extraction(xy, landmark_number, landmarks, state, thr=20.0, trials=
     if rc != 0:
         raise RuntimeError("oracle landmark_extraction rc=%d" % rc)
     return mask[:n], yproj[:n], model_dict(m), array_to_landmarks(arr, count.value)
+
+
+def set_tolerances(tol_a=0.1, tol_b=10.0, tol_dist=100.0):
+    """landmarking.py:4-6 constants used by the association walk (defaults = the reference's)."""
+    lib().or_set_tolerances(float(tol_a), float(tol_b), float(tol_dist))
+
+
+def associate(landmarks, F, cap):
+    """ransac_functions.py:34-54 walk + check_ransac's append for an already
+    fitted line F = {a, b, pos, end, id}.  Returns (match index or -1 / -2 if
+    the list was full, matched landmark dict or None, new list)."""
+    arr = landmarks_to_array(landmarks, cap)
+    f = landmarks_to_array([dict(F, life=0)], 1)
+    count = C.c_int32(len(landmarks))
+    nf = C.c_int32(0)
+    pa, pb = C.c_double(0), C.c_double(0)
+    m = lib().or_associate(arr, C.byref(count), int(cap), f, C.byref(nf), C.byref(pa), C.byref(pb))
+    matched = dict(landmarks[m]) if m >= 0 else None
+    return m, matched, array_to_landmarks(arr, count.value)
 
 
 def run_batch(xy, scan_chunk_off, chunk_pt_off, seeds, thr=20.0, trials=100, landmarks_in=None):

@@ -350,9 +350,12 @@ typedef struct {
 } or_landmark;
 
 #define OR_LIFE 40
-#define OR_TOL_A 0.1
-#define OR_TOL_B 10.0
-#define OR_TOL 100.0
+/* landmarking.py:4-6 TOLERANCE_A / TOLERANCE_B / TOLERANCE (module constants;
+ * settable like lslam_ransac_params.tol_* for the map tests) */
+static double OR_TOL_A = 0.1, OR_TOL_B = 10.0, OR_TOL = 100.0;
+void or_set_tolerances(double tol_a, double tol_b, double tol_dist) {
+    OR_TOL_A = tol_a; OR_TOL_B = tol_b; OR_TOL = tol_dist;
+}
 
 static inline double norm2(double vx, double vy) { return sqrt(fma(vy, vy, vx * vx)); }
 
