@@ -87,7 +87,9 @@ enum {
      * wall, so the chunk's own origin is not pos_j's re-observation); update (if UPDATE and >= 1
      * match) with those measurements only.  ukf_z / ukf_lmk are not read; n_landmarks = measurement slots, one per
      * chunk of a scan (>= max_scan_chunks); R_diag[2c], R_diag[2c+1] is slot c's noise.
-     * models[c] keeps the robot-frame fit; proj_a/proj_b (y_proj) stay the chunk's own line. */
+     * models[c] keeps the robot-frame fit; proj_a/proj_b (y_proj) stay the chunk's own line.
+     * id_base (if given) is in/out in this mode: advanced by the scan's chunk count, as
+     * check_ransac's landmarkNumber (ransac_functions.py:77), so steps chain without host syncs. */
     LSLAM_UKF_MAP = 8
 };
 

@@ -855,6 +855,8 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         if (lane == 0) {
             for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = mx[i];
             for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = mP[i];
+            // landmarkNumber += 1 per chunk (ransac_functions.py:77): the map's id source is in/out
+            if (B.id_base) const_cast<int32_t *>(B.id_base)[s] = id0 + nchunks;
         }
     }
     // ---- UKF step (U1-U8)

@@ -78,7 +78,8 @@ class LandmarkMap:
                                      philox_seed=self.philox_seed, tol_a=float(tol_a), tol_b=float(tol_b),
                                      tol_dist=float(tol_dist))
         self.id_next = np.zeros(R, np.int64)   # landmarkNumber per robot (check_ransac :66, :77)
-        self._id_base = ctx.empty(R, np.int32)
+        self._id_base = ctx.empty(R, np.int32)  # in/out: the kernel advances it per chunk (MAP mode)
+        self._id_base.fill_zero()
         self._caps = {}
 
     def _buf(self, name, shape, dtype):
@@ -89,9 +90,25 @@ class LandmarkMap:
             self._caps[name] = b
         return b
 
-    def step(self, xy, scan_chunk_off, chunk_pt_off, u=None, sync=True):
-        """One revolution per robot: scan r = chunks scan_chunk_off[r]:[r+1]."""
+    def upload(self, xy, scan_chunk_off, chunk_pt_off):
+        """Stage one step's revolutions in HBM (reusable by ``step``)."""
+        sco = np.ascontiguousarray(scan_chunk_off, np.int32)
+        cpo = np.ascontiguousarray(chunk_pt_off, np.int32)
+        P = int(cpo[-1])
+        inp = MapInput()
+        inp.sco, inp.cpo = sco, cpo
+        inp.xy = xy if isinstance(xy, DeviceArray) else self.ctx.to_device(
+            np.ascontiguousarray(xy, np.float64).reshape(-1, 2)[:max(P, 1)])
+        inp.dsco, inp.dcpo = self.ctx.to_device(sco), self.ctx.to_device(cpo)
+        return inp
+
+    def step(self, xy, scan_chunk_off=None, chunk_pt_off=None, u=None, sync=True):
+        """One revolution per robot: scan r = chunks scan_chunk_off[r]:[r+1].
+        ``xy`` may be a ``MapInput`` from ``upload`` (CSR arguments then omitted)."""
         ctx = self.ctx
+        staged = xy if isinstance(xy, MapInput) else None
+        if staged is not None:
+            xy, scan_chunk_off, chunk_pt_off = staged.xy, staged.sco, staged.cpo
         sco = np.ascontiguousarray(scan_chunk_off, np.int32)
         cpo = np.ascontiguousarray(chunk_pt_off, np.int32)
         if len(sco) != self.R + 1:
@@ -112,13 +129,16 @@ class LandmarkMap:
                 raise ValueError("xy holds fewer points than chunk_pt_off describes")
             dxy = self._buf("xy", (max(P, 1), 2), np.float64)
             dxy.upload(_pad(h[:P], dxy.shape[0]))
-        dsco = self._buf("sco", (self.R + 1,), np.int32)
-        dsco.upload(_pad(sco, dsco.shape[0]))
-        dcpo = self._buf("cpo", (Cn + 1,), np.int32)
-        dcpo.upload(_pad(cpo, dcpo.shape[0]))
+        if staged is not None:
+            dsco, dcpo = staged.dsco, staged.dcpo
+        else:
+            dsco = self._buf("sco", (self.R + 1,), np.int32)
+            dsco.upload(_pad(sco, dsco.shape[0]))
+            dcpo = self._buf("cpo", (Cn + 1,), np.int32)
+            dcpo.upload(_pad(cpo, dcpo.shape[0]))
         if u is not None:
             self.u.upload(np.ascontiguousarray(u, np.float64).reshape(self.R, 2))
-        self._id_base.upload(self.id_next.astype(np.int32))
+
         self.mask = self._buf("mask", (max(P, 1),), np.uint8)
         self.models = self._buf("models", (max(Cn, 1),), MODEL_DTYPE)
         b = _lib.ScanBatch()
@@ -172,6 +192,11 @@ class LandmarkMap:
             L.life = int(e["life"])
             out.append(L)
         return out
+
+
+class MapInput:
+    """One step's revolutions staged in HBM (``LandmarkMap.upload``)."""
+    xy = dsco = dcpo = sco = cpo = None
 
 
 def _pad(a, n):
