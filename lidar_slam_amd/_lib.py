@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblidarslam.so")
+LIB_PATH = os.environ.get("LSLAM_LIB") or os.path.join(_HERE, "liblidarslam.so")  # override: experiments
 
 # ---- constants mirrored from include/lidarslam.h ----
 LSLAM_OK = 0

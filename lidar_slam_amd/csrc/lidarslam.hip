@@ -75,6 +75,7 @@ struct KArgs {
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
+    int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
@@ -893,8 +894,23 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 // CU (launch_cap): they then fill the issue slots the producer's chains leave
 // idle instead of competing with them for residency (which made the producer's
 // placement, and so the step time, vary from run to run).
+// Two register budgets for the same body.  Left alone the compiler spends all
+// 512 registers of a lone wave on the UKF (occupancy 1): right beside the MT
+// producer (parity mode) that is what runs best, one post wave per SIMD taking
+// few issue slots from the parsers.  Without the producer (Philox / explicit
+// hypotheses, the stand-alone entry points) the waves_per_eu(4) build keeps a
+// batch's 4 waves per SIMD resident: fused post pass 181 -> 88 us on C3.
 template <int HYP, int MODE>
 __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);
+    for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
+        scan_body<HYP, MODE>(a, s, smem);
+        __syncthreads();
+    }
+}
+template <int HYP, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void scan_kernel_w4(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
         scan_body<HYP, MODE>(a, s, smem);
@@ -1034,6 +1050,7 @@ __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
     const uint32_t D = (uint32_t)a.T + 1u;
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
@@ -1116,6 +1133,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
 template <int HYP>
 __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if ((a.cons_prio >> 2) & 3) set_prio_level((a.cons_prio >> 2) & 3);
     for (int c = blockIdx.x; c < a.b.n_chunks; c += gridDim.x) {
         chunk_body<HYP>(a, c, smem);
         __syncthreads();
@@ -1603,6 +1621,10 @@ struct lslam_ctx {
     hipEvent_t ev_produced;      // on pstream, after rng_kernel
     hipEvent_t ev_copy;          // on stream, after the latest lslam_h2d / lslam_memset
     hipEvent_t ev_call;          // on stream, at the end of the latest pipeline call
+    // A UKF step that does not read the call's RANSAC results runs on its own
+    // stream beside the RANSAC chain; the main stream joins it before ev_call.
+    hipStream_t ustream;
+    hipEvent_t ev_ukf;           // on ustream, after the side UKF
     // buffers written by the latest pipeline call (producer inputs must not alias them)
     const void *out_ptr[12];
     size_t out_len[12];
@@ -1678,6 +1700,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
         if (v > 0) c->consumer_wgs = v;
     }
     c->pstream = nullptr;
+    c->ustream = nullptr;
     c->pslot[0] = c->pslot[1] = nullptr;
     c->pslot_bytes = 0;
     c->next_slot = 0;
@@ -1710,6 +1733,8 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[0], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[1], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_ukf, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_slot_free[0], c->stream));
@@ -1730,15 +1755,17 @@ int lslam_ctx_destroy(lslam_ctx *c) {
             if (c->ev1[k][r]) (void)hipEventDestroy(c->ev1[k][r]);
         }
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
+    if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     if (c->scr) (void)hipFree(c->scr);
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
     for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
-    hipEvent_t evs[5] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call};
+    hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
     if (c->pstream) (void)hipStreamDestroy(c->pstream);
+    if (c->ustream) (void)hipStreamDestroy(c->ustream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -1748,6 +1775,7 @@ int lslam_sync(lslam_ctx *c) {
     if (!c) return LSLAM_ERR_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->pstream));
+    HIPCHK(hipStreamSynchronize(c->ustream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return LSLAM_OK;
 }
@@ -1963,6 +1991,15 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
 #ifdef LSLAM_STAMPS
     k.dbg = g_dbg;
 #endif
+    static const int cons_prio = [] {
+        // LSLAM_CONS_PRIO="PCR": post, chunk, resolve wave priorities (digits 0-3)
+        // default "033": resolve and consensus (the chain the next producer waits on) issue
+        // ahead of the parsers' lower levels; the long post pass stays below them
+        const char *e = getenv("LSLAM_CONS_PRIO");
+        if (!e || strlen(e) != 3) e = "033";
+        return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4);
+    }();
+    k.cons_prio = cons_prio;
     k.b = *b;
     if (p) {
         if (p->min_samples != 2) return set_err(LSLAM_ERR_UNSUPPORTED, "only min_samples == 2 (ransac_functions.py:11)");
@@ -2078,10 +2115,17 @@ static int run_scan_kernel(lslam_ctx *c, const KArgs &k, int lds, int timer) {
         (void)hipFuncSetAttribute((const void *)scan_kernel<0, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         (void)hipFuncSetAttribute((const void *)scan_kernel<1, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         (void)hipFuncSetAttribute((const void *)scan_kernel<2, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
     int st = timer_begin(c, timer);
     if (st) return st;
-    HIPCHK(launch_mode<MODE>(k, lds, c->stream));
+    if (MODE == MODE_ASSOC || MODE == MODE_UKF) {  // stand-alone association / UKF: no producer beside them
+        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), dim3((unsigned)k.b.n_scans), dim3(64), lds,
+                           c->stream, k);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(launch_mode<MODE>(k, lds, c->stream));
+    }
     st = timer_end(c, timer);
     if (st) return st;
     return LSLAM_OK;
@@ -2388,9 +2432,15 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
 template <int MODE>
 static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
     static std::once_flag once;
-    std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>); });
-    hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), dim3(launch_cap(c, k.b.n_scans)), dim3(64), lds, c->stream,
-                       k);
+    std::call_once(once, [] {
+        set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>);
+        set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
+    });
+    const dim3 grid(launch_cap(c, k.b.n_scans));
+    if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
+        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
+    else
+        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     HIPCHK(hipGetLastError());
     return LSLAM_OK;
 }
@@ -2414,18 +2464,42 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     }
     KArgs kp;
     int lds_post = 0;
-    const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u ? MODE_UKF : 0);
-    if (assoc || u) {
-        st = build_args(kp, b, p, u, pmode, lds_post);
+    // a UKF step that reads nothing of this call's RANSAC (no LMK_FROM_RANSAC / MAP) runs
+    // on the side stream, off the resolve -> consensus -> association chain
+    // (Philox / explicit hypotheses only: beside the MT producer a third stream of UKF waves
+    // slows the resolve -> consensus chain more than it saves, 1.23 -> 1.27-1.32 ms on C3)
+    const bool ukf_side = p->hyp_source != LSLAM_HYP_MT19937 && u &&
+                          !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
+    const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u && !ukf_side ? MODE_UKF : 0);
+    if (assoc || (u && !ukf_side)) {
+        st = build_args(kp, b, p, ukf_side ? nullptr : u, pmode, lds_post);
+        if (st) return st;
+    }
+    KArgs ku;
+    int lds_u = 0;
+    if (ukf_side) {
+        st = build_args(ku, b, nullptr, u, MODE_UKF, lds_u);
         if (st) return st;
     }
     st = timer_begin(c, LSLAM_K_PIPELINE);
     if (st) return st;
+    if (ukf_side) {
+        // after the previous call (its outputs may be this step's inputs) and the latest copies
+        HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_call, 0));
+        HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_copy, 0));
+        static std::once_flag once;
+        std::call_once(once, [] { set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>); });
+        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_u,
+                           c->ustream, ku);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev_ukf, c->ustream));
+    }
     if (mt) {
         // producer on its own stream: it waits for its slot's previous consumers, for input
         // copies, and (on a hazard) for the previous call; the consumers wait for it
-        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
-        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
+        static const int dbg_wait = getenv("LSLAM_DBG_WAIT") ? atoi(getenv("LSLAM_DBG_WAIT")) : 3;
+        if (dbg_wait & 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
+        if (dbg_wait & 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
         if (producer_hazard(c, b)) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
         KArgs kr = k;
         kr.b.mt_state_out = k.state_scr;
@@ -2455,6 +2529,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
+    if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
     HIPCHK(hipEventRecord(c->ev_call, c->stream));
     return timer_end(c, LSLAM_K_PIPELINE);

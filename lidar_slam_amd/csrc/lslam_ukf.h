@@ -30,8 +30,17 @@ constexpr double LS_PI = 3.141592653589793;
 constexpr double LS_TWO_PI = 6.283185307179586;
 
 // UKFMethods.py:10-14 normalize_angle: Python float % (floor-mod), then -2pi above pi
+// fmod(a, 2pi) is exact; for |a| < 4pi it is a itself or a -+ 2pi (Sterbenz: exact
+// too), so the library call is only needed for far-out angles.
+__device__ __forceinline__ double fmod_two_pi(double a) {
+    const double x = fabs(a);
+    if (x < LS_TWO_PI) return a;
+    if (x < 2.0 * LS_TWO_PI) return a < 0.0 ? a + LS_TWO_PI : a - LS_TWO_PI;
+    return fmod(a, LS_TWO_PI);
+}
+
 __device__ __forceinline__ double wrap_angle(double a) {
-    double m = fmod(a, LS_TWO_PI);
+    double m = fmod_two_pi(a);
     if (m != 0.0) {
         if (m < 0.0) m += LS_TWO_PI;
     } else {
@@ -57,13 +66,18 @@ struct UkfLds {
     double *aug;   // [7][14]  [M | I] -> [I | M^-1]
     double *G;     // [28]
     double *bv;    // [7]
-    double *xv;    // [16] x(3) P(9) misc
-    double *Y;     // [7][2L] measurement residuals rz_k
+    double *xv;    // [16] misc: M^-1 b (7), K y (3)
+    double *tw;    // [7][2] predict: Wm_k sin(theta_k), Wm_k cos(theta_k)
+    double *T;     // [7][3] (W - M^-1) Dx
+    double *Y;     // [7][2L] measurement sigmas, then residuals rz_k
     double *yr;    // [2L] innovation residual_h(z, zp)
-    static __host__ __device__ int doubles(int L) { return 21 + 21 + 98 + 28 + 7 + 16 + 7 * 2 * L + 2 * L; }
+    double *wsc;   // [7][2L] Wm_k sin(phi_kj), Wm_k cos(phi_kj)
+    static __host__ __device__ int doubles(int L) {
+        return 21 + 21 + 98 + 28 + 7 + 16 + 14 + 21 + 7 * 2 * L + 2 * L + 7 * 2 * L;
+    }
     __device__ void carve(double *base, int L) {
-        sig = base; Dx = sig + 21; aug = Dx + 21; G = aug + 98; bv = G + 28; xv = bv + 7; Y = xv + 16;
-        yr = Y + 7 * 2 * L;
+        sig = base; Dx = sig + 21; aug = Dx + 21; G = aug + 98; bv = G + 28; xv = bv + 7; tw = xv + 16;
+        T = tw + 14; Y = T + 21; yr = Y + 7 * 2 * L; wsc = yr + 2 * L;
     }
 };
 
@@ -109,6 +123,12 @@ __device__ __forceinline__ void fx(const double s[3], double dt, double u0, doub
 // rows of Y and y are zero, so it adds exactly nothing to G = Y R^-1 Y^T and
 // b = Y R^-1 y (the update equals one over the active measurements alone).
 // Returns false if a factorisation failed (non-SPD P or singular M).
+//
+// Work is spread over lanes and exchanged through LDS (one wave per scan is
+// latency-bound): sigma points on lanes 0..6, hx on (sigma, landmark) pairs,
+// per-landmark means on landmark lanes, the 7x7 products on entry lanes.  Loops
+// stay rolled so the kernel keeps a few waves per SIMD resident.  Every sum runs
+// in the sigma index order k = 0..6 of the sequential form.
 template <typename LmkFn>
 __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const double *z, const double *Rd,
                          LmkFn lmk, const UkfConst &C, int flags, UkfLds &S, int lane) {
@@ -127,27 +147,31 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             S.sig[3 * lane] = o[0];
             S.sig[3 * lane + 1] = o[1];
             S.sig[3 * lane + 2] = o[2];
+            S.tw[2 * lane] = sin(o[2]) * C.Wm[lane];
+            S.tw[2 * lane + 1] = cos(o[2]) * C.Wm[lane];
         }
         __syncthreads();
         // UKFMethods.py:37-45 state_mean (intended form)
         double s0 = 0.0, s1 = 0.0, ss = 0.0, sc = 0.0;
+#pragma unroll 1
         for (int k = 0; k < 7; k++) {
-            const double a0 = S.sig[3 * k], a1 = S.sig[3 * k + 1], a2 = S.sig[3 * k + 2];
-            s0 += a0 * C.Wm[k];
-            s1 += a1 * C.Wm[k];
-            ss += sin(a2) * C.Wm[k];
-            sc += cos(a2) * C.Wm[k];
+            s0 += S.sig[3 * k] * C.Wm[k];
+            s1 += S.sig[3 * k + 1] * C.Wm[k];
+            ss += S.tw[2 * k];
+            sc += S.tw[2 * k + 1];
         }
         const double xm0 = s0, xm1 = s1, xm2 = atan2(ss, sc);
         // unscented_transform with residual_x (loop form) + Q
         double Pn[9];
         for (int i = 0; i < 9; i++) Pn[i] = 0.0;
+#pragma unroll 1
         for (int k = 0; k < 7; k++) {
             const double y0 = S.sig[3 * k] - xm0, y1 = S.sig[3 * k + 1] - xm1;
             const double y2 = wrap_angle(S.sig[3 * k + 2] - xm2);
             const double y[3] = {y0, y1, y2};
+            const double w = C.Wc[k];
             for (int i = 0; i < 3; i++)
-                for (int j = 0; j < 3; j++) Pn[3 * i + j] = Pn[3 * i + j] + C.Wc[k] * (y[i] * y[j]);
+                for (int j = 0; j < 3; j++) Pn[3 * i + j] = Pn[3 * i + j] + w * (y[i] * y[j]);
         }
         for (int i = 0; i < 9; i++) P[i] = Pn[i] + C.Q[i];
         x[0] = xm0;
@@ -174,41 +198,59 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         S.Dx[3 * lane + 2] = wrap_angle(sg[2] - x[2]);
     }
     __syncthreads();
-    // ---- hx over landmarks (lanes), z_mean, residuals -> Y, yr
     const int m2 = 2 * C.L;
-    for (int j0 = 0; j0 < C.L; j0 += 64) {
-        const int j = j0 + lane;
-        if (j < C.L) {
-            double px, py;
-            if (!lmk(j, px, py)) {
-                for (int k = 0; k < 7; k++) {
-                    S.Y[k * m2 + 2 * j] = 0.0;
-                    S.Y[k * m2 + 2 * j + 1] = 0.0;
-                }
-                S.yr[2 * j] = 0.0;
-                S.yr[2 * j + 1] = 0.0;
-                continue;
-            }
-            double d[7], ph[7];
-            for (int k = 0; k < 7; k++) {
-                const double dx = px - S.sig[3 * k], dy = py - S.sig[3 * k + 1];
-                d[k] = cr_sqrt(dx * dx + dy * dy);
-                ph[k] = wrap_angle(atan2(dy, dx) - S.sig[3 * k + 2]);
-            }
-            double dm = 0.0, ss = 0.0, sc = 0.0;
-            for (int k = 0; k < 7; k++) {
-                dm += d[k] * C.Wm[k];
-                ss += sin(ph[k]) * C.Wm[k];
-                sc += cos(ph[k]) * C.Wm[k];
-            }
-            const double pm = atan2(ss, sc);
-            for (int k = 0; k < 7; k++) {
-                S.Y[k * m2 + 2 * j] = d[k] - dm;
-                S.Y[k * m2 + 2 * j + 1] = wrap_angle(ph[k] - pm);
-            }
-            S.yr[2 * j] = z[2 * j] - dm;
-            S.yr[2 * j + 1] = wrap_angle(z[2 * j + 1] - pm);
+    const int npair = 7 * C.L;
+    // ---- hx on (sigma k, landmark j) pairs: distance, bearing, Wm-weighted sin/cos
+#pragma unroll 1
+    for (int e = lane; e < npair; e += 64) {
+        const int k = e / C.L, j = e - k * C.L;
+        double px, py;
+        double d = 0.0, ph = 0.0;
+        if (lmk(j, px, py)) {
+            const double dx = px - S.sig[3 * k], dy = py - S.sig[3 * k + 1];
+            d = cr_sqrt(dx * dx + dy * dy);
+            ph = wrap_angle(atan2(dy, dx) - S.sig[3 * k + 2]);
         }
+        S.Y[k * m2 + 2 * j] = d;
+        S.Y[k * m2 + 2 * j + 1] = ph;
+        S.wsc[k * m2 + 2 * j] = sin(ph) * C.Wm[k];
+        S.wsc[k * m2 + 2 * j + 1] = cos(ph) * C.Wm[k];
+    }
+    __syncthreads();
+    // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals
+#pragma unroll 1
+    for (int j = lane; j < C.L; j += 64) {
+        double px, py;
+        if (!lmk(j, px, py)) {
+            S.yr[2 * j] = 0.0;
+            S.yr[2 * j + 1] = 0.0;
+            continue;
+        }
+        double dm = 0.0, ss = 0.0, sc = 0.0;
+        for (int k = 0; k < 7; k++) {
+            dm += S.Y[k * m2 + 2 * j] * C.Wm[k];
+            ss += S.wsc[k * m2 + 2 * j];
+            sc += S.wsc[k * m2 + 2 * j + 1];
+        }
+        const double pm = atan2(ss, sc);
+        S.wsc[2 * j] = dm;  // row 0 of wsc is consumed: (dm, pm) per landmark
+        S.wsc[2 * j + 1] = pm;
+        S.yr[2 * j] = z[2 * j] - dm;
+        S.yr[2 * j + 1] = wrap_angle(z[2 * j + 1] - pm);
+    }
+    __syncthreads();
+    // ---- residuals rz_k on the pairs (inactive slots -> 0)
+#pragma unroll 1
+    for (int e = lane; e < npair; e += 64) {
+        const int k = e / C.L, j = e - k * C.L;
+        double px, py;
+        double r0 = 0.0, r1 = 0.0;
+        if (lmk(j, px, py)) {
+            r0 = S.Y[k * m2 + 2 * j] - S.wsc[2 * j];
+            r1 = wrap_angle(S.Y[k * m2 + 2 * j + 1] - S.wsc[2 * j + 1]);
+        }
+        S.Y[k * m2 + 2 * j] = r0;
+        S.Y[k * m2 + 2 * j + 1] = r1;
     }
     __syncthreads();
     // ---- G = Y R^-1 Y^T (28 upper entries, lanes 0..27), b = Y R^-1 y (lanes 28..34)
@@ -226,6 +268,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         double acc = 0.0;
         const double *yk = S.Y + k * m2;
         const double *yl = (l >= 0) ? S.Y + l * m2 : S.yr;
+#pragma unroll 1
         for (int m = 0; m < m2; m++) acc += (yk[m] / Rd[m]) * yl[m];
         if (lane < 28) S.G[lane] = acc;
         else S.bv[lane - 28] = acc;
@@ -247,6 +290,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
     }
     __syncthreads();
     // ---- Gauss-Jordan with partial pivoting, lanes over entries
+#pragma unroll 1
     for (int c = 0; c < 7; c++) {
         int piv = c;
         double best = fabs(S.aug[c * 14 + c]);
@@ -293,33 +337,34 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         __syncthreads();
     }
     // Minv[k][l] = aug[k*14 + 7 + l]
-    // ---- x += Dx^T M^-1 b ;  P -= Dx^T (W - M^-1) Dx
-    double mb[7];
-    for (int k = 0; k < 7; k++) {
-        double s = 0.0;
-        for (int l = 0; l < 7; l++) s += S.aug[k * 14 + 7 + l] * S.bv[l];
-        mb[k] = s;
-    }
-    double dxn[3];
-    for (int i = 0; i < 3; i++) {
-        double s = 0.0;
-        for (int k = 0; k < 7; k++) s += S.Dx[3 * k + i] * mb[k];
-        dxn[i] = s;
-    }
-    double KSK[9];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            double s = 0.0;
-            for (int k = 0; k < 7; k++) {
-                double t = 0.0;
-                for (int l = 0; l < 7; l++) {
-                    const double wml = ((k == l) ? C.Wc[k] : 0.0) - S.aug[k * 14 + 7 + l];
-                    t += wml * S.Dx[3 * l + j];
-                }
-                s += S.Dx[3 * k + i] * t;
-            }
-            KSK[3 * i + j] = s;
+    // ---- x += Dx^T M^-1 b ;  P -= Dx^T (W - M^-1) Dx  (entry lanes, LDS exchange)
+    if (lane < 7) {  // mb[k] = sum_l Minv[k][l] b[l]
+        double sacc = 0.0;
+        for (int l = 0; l < 7; l++) sacc += S.aug[lane * 14 + 7 + l] * S.bv[l];
+        S.xv[lane] = sacc;
+    } else if (lane >= 32 && lane < 32 + 21) {  // T[k][j] = sum_l (W - Minv)[k][l] Dx[l][j]
+        const int e = lane - 32, k = e / 3, j = e - 3 * k;
+        double t = 0.0;
+        for (int l = 0; l < 7; l++) {
+            const double wml = ((k == l) ? C.Wc[k] : 0.0) - S.aug[k * 14 + 7 + l];
+            t += wml * S.Dx[3 * l + j];
         }
+        S.T[e] = t;
+    }
+    __syncthreads();
+    double dxn[3], KSK[9];
+    for (int i = 0; i < 3; i++) {
+        double sacc = 0.0;
+        for (int k = 0; k < 7; k++) sacc += S.Dx[3 * k + i] * S.xv[k];
+        dxn[i] = sacc;
+    }
+#pragma unroll 1
+    for (int e = 0; e < 9; e++) {
+        const int i = e / 3, j = e - 3 * i;
+        double sacc = 0.0;
+        for (int k = 0; k < 7; k++) sacc += S.Dx[3 * k + i] * S.T[3 * k + j];
+        KSK[e] = sacc;
+    }
     for (int i = 0; i < 3; i++) x[i] = x[i] + dxn[i];
     for (int i = 0; i < 9; i++) P[i] = P[i] - KSK[i];
     __syncthreads();
