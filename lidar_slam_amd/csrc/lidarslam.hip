@@ -1629,6 +1629,10 @@ struct lslam_ctx {
     const void *out_ptr[12];
     size_t out_len[12];
     int n_out;
+    // the latest call's mt_state_out, complete once ev_slot_free[prev_slot] (after its fix-up) fired
+    const void *prev_state_out;
+    int prev_slot;
+    int prev_fixed;
 };
 
 static thread_local std::string g_err;
@@ -2287,14 +2291,18 @@ static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
 }
 
 // does the producer of this call read anything the previous pipeline call wrote?
-static bool producer_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
-    if (b->mt_state_in) return true;  // typically the previous call's mt_state_out
-    const void *in[3] = {b->seeds, b->scan_chunk_off, b->chunk_pt_off};
-    const size_t len[3] = {(size_t)b->n_scans * 4, (size_t)(b->n_scans + 1) * 4, (size_t)(b->n_chunks + 1) * 4};
-    for (int i = 0; i < 3; i++)
+// 0: no; 1: only the previous call's mt_state_out (final once that call's fix-up ran:
+// a chained stream, e.g. LandmarkMap steps); 2: something else (wait for the whole call)
+static int producer_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
+    const void *in[4] = {b->seeds, b->scan_chunk_off, b->chunk_pt_off, b->mt_state_in};
+    const size_t len[4] = {(size_t)b->n_scans * 4, (size_t)(b->n_scans + 1) * 4, (size_t)(b->n_chunks + 1) * 4,
+                           (size_t)b->n_scans * 625 * 4};
+    int level = 0;
+    for (int i = 0; i < 4; i++)
         for (int j = 0; j < c->n_out; j++)
-            if (ranges_overlap(in[i], len[i], c->out_ptr[j], c->out_len[j])) return true;
-    return false;
+            if (ranges_overlap(in[i], len[i], c->out_ptr[j], c->out_len[j]))
+                level = max(level, (i == 3 && c->out_ptr[j] == c->prev_state_out && c->prev_fixed) ? 1 : 2);
+    return level;
 }
 
 static void remember_outputs(lslam_ctx *c, const lslam_scan_batch *b, int T, int L) {
@@ -2500,7 +2508,9 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         static const int dbg_wait = getenv("LSLAM_DBG_WAIT") ? atoi(getenv("LSLAM_DBG_WAIT")) : 3;
         if (dbg_wait & 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
         if (dbg_wait & 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
-        if (producer_hazard(c, b)) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
+        const int hz = producer_hazard(c, b);
+        if (hz == 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
+        if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
         KArgs kr = k;
         kr.b.mt_state_out = k.state_scr;
         st = launch_rng(c, kr, c->pstream);
@@ -2522,6 +2532,10 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     }
+    // (mt_state_out is final after the fix-up: the next call's producer may chain from it early)
+    c->prev_state_out = mt ? b->mt_state_out : nullptr;
+    c->prev_slot = slot;
+    c->prev_fixed = mt ? 1 : 0;
     switch (pmode) {
         case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post); break;
         case MODE_POST | MODE_UKF: st = launch_post<MODE_POST | MODE_UKF>(c, kp, lds_post); break;

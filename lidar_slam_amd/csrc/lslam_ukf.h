@@ -50,6 +50,13 @@ __device__ __forceinline__ double wrap_angle(double a) {
     return m;
 }
 
+// The library's FP64 sin / cos / atan2 inline a large-argument reduction each;
+// inlined at every UKF call site they pushed the scan kernels past 256 VGPRs
+// (occupancy 1, scratch spills).  Out of line, each is one call.
+__device__ __attribute__((noinline)) double ukf_sin(double x) { return sin(x); }
+__device__ __attribute__((noinline)) double ukf_cos(double x) { return cos(x); }
+__device__ __attribute__((noinline)) double ukf_atan2(double y, double x) { return atan2(y, x); }
+
 struct UkfConst {
     double Wm[7], Wc[7];
     double cfac;  // lambda + n
@@ -67,11 +74,11 @@ struct UkfLds {
     double *G;     // [28]
     double *bv;    // [7]
     double *xv;    // [16] misc: M^-1 b (7), K y (3)
-    double *tw;    // [7][2] predict: Wm_k sin(theta_k), Wm_k cos(theta_k)
+    double *tw;    // [7][2] predict: Wm_k ukf_sin(theta_k), Wm_k ukf_cos(theta_k)
     double *T;     // [7][3] (W - M^-1) Dx
     double *Y;     // [7][2L] measurement sigmas, then residuals rz_k
     double *yr;    // [2L] innovation residual_h(z, zp)
-    double *wsc;   // [7][2L] Wm_k sin(phi_kj), Wm_k cos(phi_kj)
+    double *wsc;   // [7][2L] Wm_k ukf_sin(phi_kj), Wm_k ukf_cos(phi_kj)
     static __host__ __device__ int doubles(int L) {
         return 21 + 21 + 98 + 28 + 7 + 16 + 14 + 21 + 7 * 2 * L + 2 * L + 7 * 2 * L;
     }
@@ -106,8 +113,8 @@ __device__ __forceinline__ void sigma_point(int k, const double x[3], const doub
 // UKFMethods.py:17-24 transition_function (intended form)
 __device__ __forceinline__ void fx(const double s[3], double dt, double u0, double u1, double wr, double wb,
                                    double o[3]) {
-    const double c = (wr / 2.0) * cos(s[2]);
-    const double sn = (wr / 2.0) * sin(s[2]);
+    const double c = (wr / 2.0) * ukf_cos(s[2]);
+    const double sn = (wr / 2.0) * ukf_sin(s[2]);
     const double k0 = (-1.0 * wr) / wb, k1 = (1.0 * wr) / wb;
     const double b0 = c * u0 + c * u1;
     const double b1 = sn * u0 + sn * u1;
@@ -147,8 +154,8 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             S.sig[3 * lane] = o[0];
             S.sig[3 * lane + 1] = o[1];
             S.sig[3 * lane + 2] = o[2];
-            S.tw[2 * lane] = sin(o[2]) * C.Wm[lane];
-            S.tw[2 * lane + 1] = cos(o[2]) * C.Wm[lane];
+            S.tw[2 * lane] = ukf_sin(o[2]) * C.Wm[lane];
+            S.tw[2 * lane + 1] = ukf_cos(o[2]) * C.Wm[lane];
         }
         __syncthreads();
         // UKFMethods.py:37-45 state_mean (intended form)
@@ -160,7 +167,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             ss += S.tw[2 * k];
             sc += S.tw[2 * k + 1];
         }
-        const double xm0 = s0, xm1 = s1, xm2 = atan2(ss, sc);
+        const double xm0 = s0, xm1 = s1, xm2 = ukf_atan2(ss, sc);
         // unscented_transform with residual_x (loop form) + Q
         double Pn[9];
         for (int i = 0; i < 9; i++) Pn[i] = 0.0;
@@ -209,12 +216,12 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         if (lmk(j, px, py)) {
             const double dx = px - S.sig[3 * k], dy = py - S.sig[3 * k + 1];
             d = cr_sqrt(dx * dx + dy * dy);
-            ph = wrap_angle(atan2(dy, dx) - S.sig[3 * k + 2]);
+            ph = wrap_angle(ukf_atan2(dy, dx) - S.sig[3 * k + 2]);
         }
         S.Y[k * m2 + 2 * j] = d;
         S.Y[k * m2 + 2 * j + 1] = ph;
-        S.wsc[k * m2 + 2 * j] = sin(ph) * C.Wm[k];
-        S.wsc[k * m2 + 2 * j + 1] = cos(ph) * C.Wm[k];
+        S.wsc[k * m2 + 2 * j] = ukf_sin(ph) * C.Wm[k];
+        S.wsc[k * m2 + 2 * j + 1] = ukf_cos(ph) * C.Wm[k];
     }
     __syncthreads();
     // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals
@@ -232,7 +239,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             ss += S.wsc[k * m2 + 2 * j];
             sc += S.wsc[k * m2 + 2 * j + 1];
         }
-        const double pm = atan2(ss, sc);
+        const double pm = ukf_atan2(ss, sc);
         S.wsc[2 * j] = dm;  // row 0 of wsc is consumed: (dm, pm) per landmark
         S.wsc[2 * j + 1] = pm;
         S.yr[2 * j] = z[2 * j] - dm;
