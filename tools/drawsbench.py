@@ -31,6 +31,7 @@ for S in SIZES:
     for _ in range(5): fn()
     ctx.sync()
     ms, n = ctx.timing(_lib.K_HYP)
+    rms, rn = ctx.timing(_lib.K_RNG)
     ctx.set_timing(False)
-    out[S] = round(ms / n, 4)
+    out[S] = {"hyp_ms": round(ms / n, 4), "rng_ms": round(rms / max(rn, 1), 4)}
 print(json.dumps(out))
