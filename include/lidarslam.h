@@ -5,8 +5,10 @@
  * Plain pointers and sizes only; no torch, no C++ types.  Every function
  * returns an int status (LSLAM_OK = 0, < 0 on error) and never aborts.
  * Device pointers are HIP device memory (lslam_malloc or any hipMalloc'd
- * buffer); work is enqueued on the context's own HIP stream and is
- * asynchronous unless stated otherwise (lslam_sync waits).
+ * buffer); work is enqueued on the context's own HIP streams and is
+ * asynchronous unless stated otherwise (lslam_sync waits for all of them).
+ * lslam_h2d / lslam_d2h / lslam_memset are ordered after every earlier call
+ * on the context (a pipeline call may finish on a side stream).
  *
  * Reference interfaces each entry point replaces (reference = /root/reference,
  * fit.py = scikit-image 0.18.3 skimage/measure/fit.py, the third-party code the

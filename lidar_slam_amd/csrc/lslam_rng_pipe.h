@@ -127,8 +127,37 @@ __device__ __forceinline__ uint32_t mbcnt_from(uint64_t m, uint32_t base) {
 // next draw boundary is d = (K-1 - sg - lane) + #rejected below the lane,
 // which v_mbcnt produces directly from R, and its Fisher-Yates index is
 // i = min(d, d+K) + 1 (unsigned; the window wraps past at most one boundary).
+#ifndef LSLAM_FP_PAIRS
+#define LSLAM_FP_PAIRS 0
+#endif
 __device__ __forceinline__ uint32_t fy_index(uint32_t d, uint32_t K) { return min(d, d + K) + 1u; }
 __device__ __forceinline__ uint32_t fy_j(uint32_t w, uint32_t i) { return w & (0xffffffffu >> __clz((int)i)); }
+
+// Store j of the accepted lanes (R = the reject ballot) without a branch: exec is
+// narrowed to ~R around one store (the compiler's form re-derives the lane's bit
+// from R with three VALU and a saveexec branch).  Full exec on entry.
+__device__ __forceinline__ void store_accepted(uint8_t *J, uint32_t idx, uint32_t v, uint64_t R) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_andn2_b64 exec, exec, %1\n\t"
+        "global_store_byte %2, %3, %4\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "s"(R), "v"(idx), "v"(v), "s"(J)
+        : "memory");
+}
+__device__ __forceinline__ void store_accepted(uint16_t *J, uint32_t idx, uint32_t v, uint64_t R) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_andn2_b64 exec, exec, %1\n\t"
+        "global_store_short %2, %3, %4\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "s"(R), "v"(idx * 2u), "v"(v), "s"(J)
+        : "memory");
+}
 
 template <bool FAST, typename JT>
 __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, JT *__restrict__ J, uint32_t N,
@@ -166,8 +195,9 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
             for (int r = 0; r < nrun; r++) {
-                // next window's words (clamped inside the block; garbage past its end is never used)
-                const uint32_t nraw = kb[min(pos + 64 + lane, MT_N - 1)];
+                // next window's words: past the block's end this reads the rest of the pipe's LDS
+                // (the other block, the flags, the next pipe) or out-of-range zeros; never used
+                const uint32_t nraw = kb[pos + 64 + lane];
                 const uint32_t w = mt_temper(raw);
                 RP_STAMP(3);
                 const uint32_t b1 = K - 1u - sg;
@@ -177,6 +207,24 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 uint32_t jv = fy_j(w, i);
                 uint64_t R = ballot(jv > i), Rp;
                 int it = 1;
+#if LSLAM_FP_PAIRS
+                // two iterations per convergence test: half the compare + branch
+                // round trips (VALU -> SGPR -> SALU -> branch) on the chain, no
+                // ballot copy; a fixed point reached after the first of the pair
+                // costs one wasted iteration
+                for (;;) {
+                    d = mbcnt_from(R, base0);
+                    i = fy_index(d, K);
+                    jv = fy_j(w, i);
+                    Rp = ballot(jv > i);
+                    d = mbcnt_from(Rp, base0);
+                    i = fy_index(d, K);
+                    jv = fy_j(w, i);
+                    R = ballot(jv > i);
+                    it += 2;
+                    if (R == Rp) break;
+                }
+#else
                 do {
                     Rp = R;
                     d = mbcnt_from(Rp, base0);
@@ -185,14 +233,14 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                     R = ballot(jv > i);
                     it++;
                 } while (R != Rp);
+#endif
                 (void)it;
                 RP_STAMP(2);
                 RP_COUNT(5, 1);
                 RP_COUNT(6, it);
-                // R is the fixed point; d, i, jv belong to it.  The lane's reject
-                // bit is read back from R: a boolean carried out of the loop would
-                // be merged with exec on every iteration.
-                if (((uint32_t)(R >> lane) & 1u) == 0u) J[g + (b1 - d)] = (JT)jv;
+                // R is the fixed point; d, i, jv belong to it: the accepted lanes
+                // (exec & ~R) store their j
+                store_accepted(J, g + (b1 - d), jv, R);
                 const uint32_t na = 64u - (uint32_t)popc64(R);
                 pos += 64;
                 g += na;
