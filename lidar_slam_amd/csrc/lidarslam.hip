@@ -76,10 +76,6 @@ struct KArgs {
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
-    // post pass on its own stream: models / masks of this call come from the slot's scratch
-    // (the next call's consensus already fills the other slot); the post pass copies them out
-    const lslam_chunk_model *src_models;
-    const uint8_t *src_mask;
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
@@ -766,20 +762,13 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
             if (have_model && ci < a.corg_cap && lane == 0) corg[ci] = make_double2(rec.ox, rec.oy);
         } else {
             // post pass: models and masks come from a previous ransac launch
-            rec = a.src_models ? a.src_models[c] : B.models[c];
+            rec = B.models[c];
             rec.landmark_id = id0 + ci;  // id_base as this pass reads it (MAP mode advances it)
             have_model = (rec.flags & LSLAM_VALID) != 0;
             if (ci < a.corg_cap && lane == 0)
                 corg[ci] = have_model ? make_double2(rec.ox, rec.oy) : make_double2(__builtin_nan(""), __builtin_nan(""));
-            if (a.src_mask) {
-                for (int p = lane; p < N; p += 64) {
-                    const uint8_t m = a.src_mask[p0 + p];
-                    mk[p] = m;
-                    if (B.inlier_mask) B.inlier_mask[p0 + p] = m;
-                }
-            } else if (MODE & MODE_ASSOC) {
+            if (MODE & MODE_ASSOC)
                 for (int p = lane; p < N; p += 64) mk[p] = B.inlier_mask[p0 + p];
-            }
             __syncthreads();
         }
 
@@ -829,7 +818,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
             }
         }
-        if (lane == 0 && B.models && (kRansac || (MODE & MODE_ASSOC) || a.src_models)) B.models[c] = rec;
+        if (lane == 0 && B.models && (kRansac || (MODE & MODE_ASSOC))) B.models[c] = rec;
         __syncthreads();
     }
 
@@ -1637,11 +1626,6 @@ struct lslam_ctx {
     // stream beside the RANSAC chain; the main stream joins it before ev_call.
     hipStream_t ustream;
     hipEvent_t ev_ukf;           // on ustream, after the side UKF
-    // Parity mode with a post pass: the post pass of call k runs on ustream beside the next
-    // call's resolve / consensus, reading the models and masks of its producer slot
-    void *cslot[2];              // per slot: lslam_chunk_model[n_chunks] + uint8 mask[n_points]
-    size_t cslot_bytes;
-    hipEvent_t ev_posted[2];     // on ustream, after the post pass that read the slot
     // buffers written by the latest pipeline call (producer inputs must not alias them)
     const void *out_ptr[12];
     size_t out_len[12];
@@ -1723,8 +1707,6 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->pstream = nullptr;
     c->ustream = nullptr;
     c->pslot[0] = c->pslot[1] = nullptr;
-    c->cslot[0] = c->cslot[1] = nullptr;
-    c->cslot_bytes = 0;
     c->pslot_bytes = 0;
     c->next_slot = 0;
     c->n_out = 0;
@@ -1758,10 +1740,6 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_ukf, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_posted[0], hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_posted[1], hipEventDisableTiming));
-    HIPCHK(hipEventRecord(c->ev_posted[0], c->ustream));
-    HIPCHK(hipEventRecord(c->ev_posted[1], c->ustream));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_slot_free[0], c->stream));
@@ -1786,12 +1764,9 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     if (c->scr) (void)hipFree(c->scr);
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
-        if (c->cslot[i]) (void)hipFree(c->cslot[i]);
-    }
-    hipEvent_t evs[8] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf,
-                         c->ev_posted[0], c->ev_posted[1]};
+    hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
     if (c->pstream) (void)hipStreamDestroy(c->pstream);
@@ -2265,26 +2240,6 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     return LSLAM_OK;
 }
 
-// Per producer slot: the consensus output (models + masks) the slot's post pass reads.
-static int ensure_cslot(lslam_ctx *c, size_t bytes) {
-    if (c->cslot_bytes >= bytes) return LSLAM_OK;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipStreamSynchronize(c->pstream));
-    HIPCHK(hipStreamSynchronize(c->ustream));
-    for (int i = 0; i < 2; i++) {
-        if (c->cslot[i]) HIPCHK(hipFree(c->cslot[i]));
-        c->cslot[i] = nullptr;
-    }
-    c->cslot_bytes = 0;
-    for (int i = 0; i < 2; i++) {
-        hipError_t e = hipMalloc(&c->cslot[i], bytes);
-        if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (consensus slot)");
-        HIPCHK(e);
-    }
-    c->cslot_bytes = bytes;
-    return LSLAM_OK;
-}
-
 // resolve_kernel LDS: the chunk's staged steps (if they fit)
 static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     if (base.b.n_chunks == 0) return LSLAM_OK;
@@ -2488,18 +2443,17 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
 }
 
 template <int MODE>
-static int launch_post(lslam_ctx *c, const KArgs &k, int lds, hipStream_t st) {
+static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
     static std::once_flag once;
     std::call_once(once, [] {
         set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>);
         set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
     const dim3 grid(launch_cap(c, k.b.n_scans));
-    static const int post_w4 = getenv("LSLAM_POST_W4") ? atoi(getenv("LSLAM_POST_W4")) : 0;
-    if (k.hyp_source == LSLAM_HYP_MT19937 && !post_w4)  // beside the next call's producer
-        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, st, k);
+    if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
+        hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     else
-        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, st, k);
+        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     HIPCHK(hipGetLastError());
     return LSLAM_OK;
 }
@@ -2540,25 +2494,6 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         st = build_args(ku, b, nullptr, u, MODE_UKF, lds_u);
         if (st) return st;
     }
-    // Optional (LSLAM_POST_STREAM=1), parity mode with a post pass: the post pass runs on
-    // ustream, so call k's association / UKF overlaps call k+1's resolve and consensus.  The
-    // consensus writes the slot's scratch models / masks, the post pass copies them to the
-    // caller's buffers.  Off by default: on C3 the chip is already shared three ways and the
-    // extra overlap cost 1.26 -> 1.28-1.30 ms.
-    static const bool ps_ok = getenv("LSLAM_POST_STREAM") && atoi(getenv("LSLAM_POST_STREAM")) != 0;
-    const bool post_stream = ps_ok && mt && (assoc || (u && !ukf_side));
-    if (post_stream) {
-        const size_t mbytes = (((size_t)(b->n_chunks > 0 ? b->n_chunks : 1) * sizeof(lslam_chunk_model)
-                                                   + 255) & ~(size_t)255);
-        st = ensure_cslot(c, mbytes + (size_t)(b->n_points > 0 ? b->n_points : 1) + 256);
-        if (st) return st;
-        lslam_chunk_model *sm = (lslam_chunk_model *)c->cslot[slot];
-        uint8_t *sk = (uint8_t *)c->cslot[slot] + mbytes;
-        k.b.models = sm;
-        k.b.inlier_mask = sk;
-        kp.src_models = sm;
-        kp.src_mask = sk;
-    }
     st = timer_begin(c, LSLAM_K_PIPELINE);
     if (st) return st;
     if (ukf_side) {
@@ -2590,8 +2525,6 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         st = launch_resolve(c, k);
         if (st) return st;
     }
-    // the slot's scratch was read by the post pass of call k-2
-    if (post_stream) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_posted[slot], 0));
     st = launch_chunks(c, k, !assoc);
     if (st) return st;
     if (mt) {
@@ -2608,26 +2541,17 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     c->prev_state_out = mt ? b->mt_state_out : nullptr;
     c->prev_slot = slot;
     c->prev_fixed = mt ? 1 : 0;
-    hipStream_t pst = c->stream;
-    if (post_stream) {
-        // after this call's fix-up (final models / masks / stream state) and the latest copies;
-        // the previous post pass is earlier on the same stream
-        HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_slot_free[slot], 0));
-        HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_copy, 0));
-        pst = c->ustream;
-    }
     switch (pmode) {
-        case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post, pst); break;
-        case MODE_POST | MODE_UKF: st = launch_post<MODE_POST | MODE_UKF>(c, kp, lds_post, pst); break;
-        case MODE_ASSOC: st = launch_post<MODE_ASSOC>(c, kp, lds_post, pst); break;
+        case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post); break;
+        case MODE_POST | MODE_UKF: st = launch_post<MODE_POST | MODE_UKF>(c, kp, lds_post); break;
+        case MODE_ASSOC: st = launch_post<MODE_ASSOC>(c, kp, lds_post); break;
         default: break;
     }
     if (st) return st;
-    if (post_stream) HIPCHK(hipEventRecord(c->ev_posted[slot], c->ustream));
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
-    HIPCHK(hipEventRecord(c->ev_call, pst));
-    return timer_end(c, LSLAM_K_PIPELINE, pst);
+    HIPCHK(hipEventRecord(c->ev_call, c->stream));
+    return timer_end(c, LSLAM_K_PIPELINE);
 }
 
 
