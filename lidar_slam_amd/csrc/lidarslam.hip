@@ -1062,6 +1062,79 @@ __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     }
 }
 
+// Chunks whose steps do not fit the 16 KiB stage (C5: 2049 draws x 4095 steps
+// x 2 B = 16.8 MB per chunk).  One wave per (chunk, group of 64 draws), lanes =
+// draws as in resolve_draws_fwd, but the steps stream through an LDS tile of
+// [64 draws][RB steps] filled with row-contiguous (coalesced) loads: a lane
+// walking its own draw straight from HBM touches 64 cache lines per load and
+// left C5's resolve at 150 ms per call.  Rows are padded to an odd number of
+// dwords, so the lanes' reads of one step column hit distinct banks.
+constexpr int RB = 128;                 // steps per tile (= 2 columns per lane in the fill)
+constexpr int RB_STRIDE = RB + 2;       // row stride in elements (u16: 65 dwords; u8: pad to 33 dwords below)
+template <typename JT>
+__global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngroups) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int STRIDE = sizeof(JT) == 2 ? RB_STRIDE : RB + 4;
+    JT *tile = (JT *)smem;
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const uint32_t D = (uint32_t)a.T + 1u;
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
+    const int64_t total = (int64_t)B.n_chunks * ngroups;
+    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
+        const int c = (int)(e / ngroups), g = (int)(e - (int64_t)c * ngroups);
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        const uint32_t K = (uint32_t)N - 1u;
+        const uint32_t d0 = (uint32_t)g * 64u;
+        const uint32_t nd = min(64u, D - d0);
+        const JT *Jc = (const JT *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)d0 * K;  // row r = draw d0 + r
+        uint32_t c0 = 0, c1 = 1;
+        // forward scan i = 2..K reads memory offset K - i: tiles of i in [i0, i0 + RB)
+        for (uint32_t i0 = 2; i0 <= K; i0 += RB) {
+            const uint32_t i1 = min(i0 + (uint32_t)RB, K + 1u);  // exclusive
+            const uint32_t mlo = K - (i1 - 1u);                  // lowest memory offset of the tile
+            const uint32_t ncol = i1 - i0;
+            // 8 rows x 2 columns per lane in flight, then into LDS
+            for (uint32_t r0 = 0; r0 < nd; r0 += 8) {
+                JT v[8][2];
+#pragma unroll
+                for (int rr = 0; rr < 8; rr++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t r = r0 + (uint32_t)rr, x = (uint32_t)lane + 64u * (uint32_t)h;
+                        v[rr][h] = (r < nd && x < ncol) ? Jc[(size_t)r * K + mlo + x] : (JT)0;
+                    }
+#pragma unroll
+                for (int rr = 0; rr < 8; rr++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t r = r0 + (uint32_t)rr, x = (uint32_t)lane + 64u * (uint32_t)h;
+                        if (r < nd && x < ncol) tile[r * STRIDE + x] = v[rr][h];
+                    }
+            }
+            __syncthreads();
+            if ((uint32_t)lane < nd) {
+                const JT *trow = tile + lane * STRIDE;
+                for (uint32_t i = i0; i < i1; i++) {
+                    const uint32_t j = trow[K - i - mlo];
+                    c0 = (j == c0) ? i : c0;
+                    c1 = (j == c1) ? i : c1;
+                }
+            }
+            __syncthreads();
+        }
+        if ((uint32_t)lane < nd) {
+            const uint32_t d = d0 + (uint32_t)lane;
+            const uint32_t j1 = Jc[(size_t)lane * K + (K - 1u)];
+            int32_t *draws = a.draws_scr + (size_t)c * 2 * D;
+            draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
+            draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------
 // chunk_kernel: one wave per chunk, A4-A8 with the draws given
 // ------------------------------------------------------------------------
@@ -2250,6 +2323,16 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     const int64_t need = ((int64_t)(k.T + 1) * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
     const int lds = need <= 16 * 1024 ? (int)need : 0;
     k.res_g = lds;  // staging capacity in bytes
+    if (lds == 0) {  // steps streamed through LDS tiles, waves over (chunk, 64 draws)
+        const int ngroups = (k.T + 1 + 63) / 64;
+        const int64_t items = (int64_t)k.b.n_chunks * ngroups;
+        const dim3 grid(launch_cap(c, items > (1 << 30) ? (1 << 30) : items)), block(64);
+        const int tl = 64 * (RB + 4) * esz;
+        if (k.j8) hipLaunchKernelGGL(resolve_big_kernel<uint8_t>, grid, block, tl, c->stream, k, ngroups);
+        else hipLaunchKernelGGL(resolve_big_kernel<uint16_t>, grid, block, tl, c->stream, k, ngroups);
+        HIPCHK(hipGetLastError());
+        return LSLAM_OK;
+    }
     static std::once_flag once;
     std::call_once(once, [] {
         set_max_lds(resolve_kernel<uint8_t>);

@@ -87,6 +87,26 @@ def _check_vs_golden(g, r):
     assert np.all(_rel(r["y_proj"][sel], g["q_y"]) < REL)
 
 
+@pytest.mark.parametrize("n,trials", [(100, 250), (200, 100), (256, 70), (300, 60), (1000, 40)])
+def test_hyp_mt19937_resolve_paths(ctx, n, trials):
+    """Draws of chunks whose steps exceed the 16 KiB LDS stage (u8 steps for N <= 256, u16
+    above): the tiled resolve_big_kernel path, chained over 3 chunks per scan, vs the
+    oracle's choice(N, 2) sequence."""
+    from lidar_slam_amd import pipeline as pl
+    seeds = [11, 12, 13]
+    S = len(seeds)
+    sizes = [n, n - 7, n + 3]
+    sco = np.arange(0, 3 * S + 1, 3, dtype=np.int32)
+    cpo = np.concatenate([[0], np.cumsum(sizes * S)]).astype(np.int32)
+    draws, state = pl.hyp_mt19937(ctx, sco, cpo, seeds=seeds, max_trials=trials)
+    for s, seed in enumerate(seeds):
+        st = orc.MTState(seed=seed)
+        for k, nk in enumerate(sizes):
+            ref = np.array([st.choice2(nk) for _ in range(trials + 1)])
+            assert np.array_equal(draws[3 * s + k], ref), (n, trials, s, k)
+        assert np.array_equal(state[s, :624], st.key) and state[s, 624] == st.pos.value
+
+
 def test_batch_pipeline_vs_reference(ctx, golden):
     g = golden("batch.npz")
     r = _run_batch(ctx, g, seeds=g["seeds"])
