@@ -127,9 +127,6 @@ __device__ __forceinline__ uint32_t mbcnt_from(uint64_t m, uint32_t base) {
 // next draw boundary is d = (K-1 - sg - lane) + #rejected below the lane,
 // which v_mbcnt produces directly from R, and its Fisher-Yates index is
 // i = min(d, d+K) + 1 (unsigned; the window wraps past at most one boundary).
-#ifndef LSLAM_FP_PAIRS
-#define LSLAM_FP_PAIRS 0
-#endif
 __device__ __forceinline__ uint32_t fy_index(uint32_t d, uint32_t K) { return min(d, d + K) + 1u; }
 __device__ __forceinline__ uint32_t fy_j(uint32_t w, uint32_t i) { return w & (0xffffffffu >> __clz((int)i)); }
 
@@ -207,24 +204,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 uint32_t jv = fy_j(w, i);
                 uint64_t R = ballot(jv > i), Rp;
                 int it = 1;
-#if LSLAM_FP_PAIRS
-                // two iterations per convergence test: half the compare + branch
-                // round trips (VALU -> SGPR -> SALU -> branch) on the chain, no
-                // ballot copy; a fixed point reached after the first of the pair
-                // costs one wasted iteration
-                for (;;) {
-                    d = mbcnt_from(R, base0);
-                    i = fy_index(d, K);
-                    jv = fy_j(w, i);
-                    Rp = ballot(jv > i);
-                    d = mbcnt_from(Rp, base0);
-                    i = fy_index(d, K);
-                    jv = fy_j(w, i);
-                    R = ballot(jv > i);
-                    it += 2;
-                    if (R == Rp) break;
-                }
-#else
                 do {
                     Rp = R;
                     d = mbcnt_from(Rp, base0);
@@ -233,7 +212,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                     R = ballot(jv > i);
                     it++;
                 } while (R != Rp);
-#endif
                 (void)it;
                 RP_STAMP(2);
                 RP_COUNT(5, 1);
