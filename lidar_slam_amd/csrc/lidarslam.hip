@@ -2593,9 +2593,8 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (mt) {
         // producer on its own stream: it waits for its slot's previous consumers, for input
         // copies, and (on a hazard) for the previous call; the consumers wait for it
-        static const int dbg_wait = getenv("LSLAM_DBG_WAIT") ? atoi(getenv("LSLAM_DBG_WAIT")) : 3;
-        if (dbg_wait & 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
-        if (dbg_wait & 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
+        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
+        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
         const int hz = producer_hazard(c, b);
         if (hz == 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
         if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
