@@ -274,6 +274,49 @@ def test_philox_and_explicit_vs_oracle(ctx, golden):
         assert r["models"]["a"][c] == md["a"] and r["models"]["best_trial"][c] == md["best_trial"]
 
 
+def test_philox_pipeline_with_side_ukf_and_assoc(ctx, golden):
+    """Philox hypotheses + association + UKF: the UKF (it reads nothing of the RANSAC) runs on
+    the side stream beside the consensus, the association pass in the waves_per_eu(4) build.
+    Two chained calls: x/P in/out vs the oracle UKF, masks/lists vs the explicit-draw path and
+    the stand-alone association entry point."""
+    from lidar_slam_amd.pipeline import ScanPipeline
+    from oracle import ukf as oukf
+    g = golden("batch.npz")
+    S = len(g["scan_chunk_off"]) - 1
+    L = 8
+    rng = np.random.default_rng(17)
+    x0 = np.column_stack([rng.uniform(500, 3500, S), rng.uniform(500, 2500, S), rng.uniform(-3, 3, S)])
+    P0 = np.tile(np.diag([.1, .1, .05]), (S, 1, 1))
+    lmk = rng.uniform(-3000, 3000, (S, L, 2))
+    z = np.stack([oukf.transfer_function(x0[s], lmk[s]) for s in range(S)]) + rng.normal(0, 0.2, (S, 2 * L))
+    u = np.tile([2.0, 2.5], (S, 1))
+    Rd = np.array([oukf.VAR_DIST, oukf.VAR_ANGLE] * L)
+    ukf = dict(n_landmarks=L, x=x0, P=P0, u=u, z=z, lmk=lmk, R_diag=Rd)
+    p = ScanPipeline(ctx, g["xy"], g["scan_chunk_off"], g["chunk_pt_off"], hyp="philox", want_draws=True,
+                     lmk_capacity=64, ukf=ukf)
+    p.run(sync=False)
+    p.run()  # the second call chains x/P from the first
+    r = p.results()
+    xo, Po = oukf.ukf_batch(x0, P0, u, z, lmk, Rd)
+    xo, Po = oukf.ukf_batch(xo, Po, u, z, lmk, Rd)
+    assert np.max(np.abs(r["ukf_x"] - xo)) <= 1e-4
+    assert np.max(np.abs(r["ukf_P"] - Po)) <= 1e-6
+    # association: the explicit path with the same draws, fresh lists, one call
+    p2 = ScanPipeline(ctx, g["xy"], g["scan_chunk_off"], g["chunk_pt_off"], hyp="explicit", hyp_draws=r["draws"],
+                      lmk_capacity=64)
+    p2.run()
+    r2 = p2.results()
+    assert np.array_equal(r2["mask"], r["mask"])
+    # stand-alone association entry point over the models of the explicit call, fresh lists
+    p2.reset_state()
+    p2.run_landmarks_only()
+    r3 = p2.results()
+    for k in ("lmk_count",):
+        assert np.array_equal(r3[k], r2[k])
+    assert np.array_equal(r3["landmarks"]["id"], r2["landmarks"]["id"])
+    assert np.array_equal(r3["y_proj"], r2["y_proj"])
+
+
 def test_polar_to_xy(ctx):
     from lidar_slam_amd import pipeline as pl
     from lidar_slam_amd import synth
