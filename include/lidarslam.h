@@ -266,7 +266,9 @@ int lslam_ransac(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_p
 int lslam_landmarks(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p);
 /* U1-U8: one predict and/or update per scan */
 int lslam_ukf_step(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ukf_params *u);
-/* A3-A10 (+ U1-U8 if u != NULL) fused: one wave per scan, one launch */
+/* A3-A10 (+ U1-U8 if u != NULL) for every scan of the batch in one call: MT19937 producer (its
+ * own stream, overlapping the previous call's consumers), resolve, consensus, fix-up, then the
+ * association / UKF post pass */
 int lslam_scan_pipeline(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p,
                         const lslam_ukf_params *u);
 

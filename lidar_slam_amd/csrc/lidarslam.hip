@@ -3,16 +3,21 @@
 // points each function replaces and DESIGN.md for the layout/roofline notes.
 //
 // Execution model (lslam_scan_pipeline, parity mode):
-//   rng_kernel     one workgroup (parser wave + helper wave) per scan: the
-//                  scan's chained legacy MT19937 stream (ransac_functions.py:73
-//                  + fit.py:791) -> every chunk's T+1 draws, assuming no early
-//                  stop (lslam_rng_pipe.h)
+//   rng_kernel     (producer stream) one parser wave per scan, 4 parsers + 1
+//                  twisting helper per workgroup: the scan's chained legacy
+//                  MT19937 stream (ransac_functions.py:73 + fit.py:791) -> the
+//                  j of every Fisher-Yates step, assuming no early stop
+//                  (lslam_rng_pipe.h)
+//   resolve_kernel one wave per chunk (resolve_big_kernel: per 64 draws when the
+//                  chunk's steps exceed the LDS stage): steps -> the T+1 draws
 //   chunk_kernel   one wave per chunk: A4/A5 counts (lane = hypothesis), A6 tie
 //                  sums + selection, mask + A7 refit, A8 line parameters
+//                  (chunks of > 128 points: model / count / select kernels)
 //   scan_kernel    (fix-up) one wave per scan; exits at once unless one of its
 //                  chunks stopped early, then replays the scan sequentially
 //   scan_kernel    (post) one wave per scan: A9/A10 association walk over the
-//                  chunks in order, y_proj, then U1-U8 UKF
+//                  chunks in order, y_proj, then U1-U8 UKF (LSLAM_UKF_MAP:
+//                  predict, world-frame association, update with the matches)
 // Philox / explicit hypotheses skip the producer and the fix-up.  A chunk's
 // points, draws and scratch live in LDS; HBM sees the points once per pass.
 //

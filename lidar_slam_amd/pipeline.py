@@ -3,8 +3,9 @@
 This is the batched entry point the reference never had: the per-chunk
 ``landmark_extraction`` (ransac_functions.py:15-59) driven by ``check_ransac``
 (ransac_functions.py:63-93) over every chunk of many scans, plus the intended
-UKF step (systemClass.py / UKFMethods.py), in ONE kernel launch
-(``lslam_scan_pipeline``).  Semantics per scan: ``np.random.seed(seed[s])``
+UKF step (systemClass.py / UKFMethods.py), in ONE library call
+(``lslam_scan_pipeline``: producer, resolve, consensus, fix-up and post-pass
+kernels on the device).  Semantics per scan: ``np.random.seed(seed[s])``
 (or an explicit MT19937 state) chained over the scan's chunks, and the scan's
 own landmark list (``landmarks[s]``), ids ``id_base[s] + chunk index``.
 """
