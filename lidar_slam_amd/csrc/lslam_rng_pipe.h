@@ -136,24 +136,29 @@ __device__ __forceinline__ uint32_t fy_j(uint32_t w, uint32_t i) { return w & (0
 __device__ __forceinline__ void store_accepted(uint8_t *J, uint32_t idx, uint32_t v, uint64_t R) {
     uint64_t saved;
     asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_andn2_b64 exec, exec, %1\n\t"
+        "s_andn1_saveexec_b64 %0, %1\n\t"  // saved = exec; exec = ~R & exec
         "global_store_byte %2, %3, %4\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
         : "s"(R), "v"(idx), "v"(v), "s"(J)
-        : "memory");
+        : "memory", "scc");
 }
 __device__ __forceinline__ void store_accepted(uint16_t *J, uint32_t idx, uint32_t v, uint64_t R) {
     uint64_t saved;
     asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_andn2_b64 exec, exec, %1\n\t"
+        "s_andn1_saveexec_b64 %0, %1\n\t"
         "global_store_short %2, %3, %4\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
         : "s"(R), "v"(idx * 2u), "v"(v), "s"(J)
-        : "memory");
+        : "memory", "scc");
+}
+
+// Accepted lanes of a full window = zero bits of the reject ballot.
+__device__ __forceinline__ uint32_t accepted_count(uint64_t R) {
+    uint32_t n;
+    asm("s_bcnt0_i32_b64 %0, %1" : "=s"(n) : "s"(R) : "scc");
+    return n;
 }
 
 template <bool FAST, typename JT>
@@ -216,10 +221,10 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 RP_STAMP(2);
                 RP_COUNT(5, 1);
                 RP_COUNT(6, it);
-                // R is the fixed point; d, i, jv belong to it: the accepted lanes
+                // R is the fixed point; d, jv belong to it: the accepted lanes
                 // (exec & ~R) store their j
                 store_accepted(J, g + (b1 - d), jv, R);
-                const uint32_t na = 64u - (uint32_t)popc64(R);
+                const uint32_t na = accepted_count(R);
                 pos += 64;
                 g += na;
                 sg += na;
