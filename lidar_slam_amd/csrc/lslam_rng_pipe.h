@@ -208,15 +208,19 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 uint32_t i = fy_index(d, K);
                 uint32_t jv = fy_j(w, i);
                 uint64_t R = ballot(jv > i), Rp;
+                int it = 1;
                 do {
                     Rp = R;
                     d = mbcnt_from(Rp, base0);
                     i = fy_index(d, K);
                     jv = fy_j(w, i);
                     R = ballot(jv > i);
+                    it++;
                 } while (R != Rp);
+                (void)it;
                 RP_STAMP(2);
                 RP_COUNT(5, 1);
+                RP_COUNT(6, it);
                 // R is the fixed point; d, jv belong to it: the accepted lanes
                 // (exec & ~R) store their j
                 store_accepted(J, g + (b1 - d), jv, R);
