@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LSLAM_ABI_VERSION 1
+#define LSLAM_ABI_VERSION 2
 
 /* ---- status codes ---- */
 enum {
@@ -153,7 +153,7 @@ typedef struct lslam_scan_batch {
     int32_t lmk_capacity;           /* per-scan landmark list capacity */
     int32_t reserved;
     /* inputs */
-    const double *xy;               /* [n_points][2] fp64 Cartesian points (AoS) */
+    const double *xy;               /* [n_points][2] fp64 Cartesian points (AoS); NULL: theta_deg / dist_mm */
     const int32_t *scan_chunk_off;  /* [n_scans+1] CSR scan -> chunks */
     const int32_t *chunk_pt_off;    /* [n_chunks+1] CSR chunk -> points */
     const uint32_t *seeds;          /* [n_scans] np.random.seed(seed) per scan (MT19937 mode) */
@@ -180,6 +180,11 @@ typedef struct lslam_scan_batch {
     const double *ukf_z;            /* [n_scans][2L] interleaved [d0, phi0, d1, phi1, ...] (not in MAP mode) */
     const double *ukf_lmk;          /* [n_scans][L][2] landmark positions (not in MAP mode) */
     const double *ukf_R_diag;       /* [2L] measurement noise diagonal (systemClass.py:28) */
+    /* A1 fused into the point loads (ABI 2): with xy == NULL the points are
+     * the raw measures and every kernel that reads a point converts it as functions.py:59-60 does,
+     * x = d cos(-th * pi/180 + pi/2), y = d sin(...), bit-identical to lslam_polar_to_xy. */
+    const double *theta_deg;        /* [n_points] */
+    const double *dist_mm;          /* [n_points] */
 } lslam_scan_batch;
 
 /* Express-scan measures (lslam_express_decode): device arrays, NULL = not written.

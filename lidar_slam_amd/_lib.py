@@ -68,7 +68,7 @@ class ScanBatch(C.Structure):
                [(n, _VP) for n in ("xy", "scan_chunk_off", "chunk_pt_off", "seeds", "mt_state_in", "mt_state_out",
                                    "hyp", "id_base", "landmarks", "lmk_count", "lmk_walk", "inlier_mask", "models", "y_proj",
                                    "draws_out", "trial_cnt_out", "ukf_x", "ukf_P", "ukf_u", "ukf_z", "ukf_lmk",
-                                   "ukf_R_diag")]
+                                   "ukf_R_diag", "theta_deg", "dist_mm")]
 
 
 class ExpressMeasures(C.Structure):

@@ -45,6 +45,40 @@
 using namespace lslam;
 
 static_assert(sizeof(lslam_chunk_model) == 112, "chunk model ABI");
+
+// functions.py:59-60 for one measure; polar_kernel and every fused point load
+// use this one definition, so both give the same bits.  Out of line: inlined
+// sin/cos in every point-staging loop slowed the xy path of C3 by 2.5 %.
+__device__ __attribute__((noinline)) double2 polar_xy(double th, double d) {
+    const double ang = -th * (LS_PI / 180.0) + LS_PI / 2.0;
+    return make_double2(d * cos(ang), d * sin(ang));
+}
+
+// A batch's points: Cartesian xy, or raw (theta, d) measures converted on load
+// (A1 fused, lslam_scan_batch.theta_deg / dist_mm).  The choice is uniform.
+struct PtSrc {
+    const double2 *xy;
+    const double *th, *dd;
+    __device__ __forceinline__ double2 operator[](int64_t i) const { return xy ? xy[i] : polar_xy(th[i], dd[i]); }
+    __device__ __forceinline__ PtSrc operator+(int64_t o) const {
+        PtSrc r = *this;
+        if (xy) r.xy += o;
+        else { r.th += o; r.dd += o; }
+        return r;
+    }
+};
+__device__ __forceinline__ PtSrc batch_points(const lslam_scan_batch &B) {
+    return PtSrc{(const double2 *)B.xy, B.theta_deg, B.dist_mm};
+}
+// a chunk's points -> LDS, the xy loop kept free of the polar path
+__device__ __forceinline__ void stage_points(const lslam_scan_batch &B, int p0, int N, double2 *P, int lane) {
+    if (B.xy) {
+        const double2 *src = (const double2 *)B.xy + p0;
+        for (int p = lane; p < N; p += 64) P[p] = src[p];
+    } else {
+        for (int p = lane; p < N; p += 64) P[p] = polar_xy(B.theta_deg[p0 + p], B.dist_mm[p0 + p]);
+    }
+}
 static_assert(sizeof(lslam_landmark) == 56, "landmark ABI");
 
 enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8, MODE_POST = 16 };
@@ -743,8 +777,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 continue;
             }
             // ---- stage the chunk's points in LDS (16 B per lane, coalesced)
-            const double2 *src = (const double2 *)B.xy + p0;
-            for (int p = lane; p < N; p += 64) P[p] = src[p];
+            stage_points(B, p0, N, P, lane);
             __syncthreads();
             // ---- A4-A7
             const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack,
@@ -818,9 +851,16 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         }
         if (B.y_proj && (kRansac || (MODE & MODE_ASSOC))) {
             const double pa = rec.proj_a, pb = rec.proj_b;
-            for (int p = lane; p < N; p += 64) {
-                const double x = B.xy[2 * (size_t)(p0 + p)];
-                B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
+            if (B.xy) {
+                for (int p = lane; p < N; p += 64) {
+                    const double x = B.xy[2 * (size_t)(p0 + p)];
+                    B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
+                }
+            } else {
+                for (int p = lane; p < N; p += 64) {
+                    const double x = polar_xy(B.theta_deg[p0 + p], B.dist_mm[p0 + p]).x;
+                    B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * x + pb) : 0.0;
+                }
             }
         }
         if (lane == 0 && B.models && (kRansac || (MODE & MODE_ASSOC))) B.models[c] = rec;
@@ -1196,8 +1236,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
     }
-    const double2 *src = (const double2 *)B.xy + p0;
-    for (int p = lane; p < N; p += 64) P[p] = src[p];
+    stage_points(B, p0, N, P, lane);
     __syncthreads();
     const ChunkOut o = chunk_consensus(a, P, N, draws, cnt, tied, tsum, inl, vtmp, vstack, nstack,
                                        B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
@@ -1247,7 +1286,8 @@ struct ChunkBox {
     bool finite;
 };
 
-__device__ __forceinline__ void box_partial(const double2 *src, int N, int tid, int nthr, double2 *P, double &xmn,
+template <typename Src>
+__device__ __forceinline__ void box_partial(const Src src, int N, int tid, int nthr, double2 *P, double &xmn,
                                             double &xmx, double &ymn, double &ymx, bool &fin) {
     xmn = __builtin_inf(); xmx = -__builtin_inf(); ymn = __builtin_inf(); ymx = -__builtin_inf();
     fin = true;
@@ -1309,7 +1349,7 @@ __global__ __launch_bounds__(256) void model_kernel(const KArgs a) {
         a.draws_scr[((size_t)c * D + t) * 2 + 1] = i1;
     }
     if (t >= T) return;
-    const double2 *xy = (const double2 *)B.xy + p0;
+    const PtSrc xy = batch_points(B) + p0;
     const Model m = model2(xy[i0], xy[i1]);
     double *o = a.models + ((size_t)c * T + t) * 4;
     *(double4 *)o = make_double4(m.ox, m.oy, m.ux, m.uy);
@@ -1336,7 +1376,7 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
         s_hi[h] = 0;
         s_ex[h] = 0;
     }
-    const double2 *xy = (const double2 *)B.xy + p0;
+    const PtSrc xy = batch_points(B) + p0;
     double xmn, xmx, ymn, ymx;
     bool fin;
     box_partial(xy, N, tid, CNT_TPB, nullptr, xmn, xmx, ymn, ymx, fin);
@@ -1504,7 +1544,7 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
         for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
     double xmn, xmx, ymn, ymx;
     bool fin;
-    box_partial((const double2 *)B.xy + p0, N, lane, 64, P, xmn, xmx, ymn, ymx, fin);
+    box_partial(batch_points(B) + p0, N, lane, 64, P, xmn, xmx, ymn, ymx, fin);
     SEL_STAMP(0);
     const ChunkBox bx = box_finish(unid(xmn), unid(xmx), unid(ymn), unid(ymx), ballot(!fin) == 0ull);
     __syncthreads();
@@ -1651,12 +1691,8 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
 // A1: polar -> Cartesian (functions.py:59-60)
 __global__ __launch_bounds__(256) void polar_kernel(const double *__restrict__ th, const double *__restrict__ d,
                                                     double2 *__restrict__ xy, int64_t n) {
-    const double A = LS_PI / 180.0;
-    const double H = LS_PI / 2.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double ang = -th[i] * A + H;
-        const double di = d[i];
-        xy[i] = make_double2(di * cos(ang), di * sin(ang));
+        xy[i] = polar_xy(th[i], d[i]);
     }
 }
 
@@ -2059,7 +2095,8 @@ static int validate_batch(const lslam_scan_batch *b, bool need_points) {
     if (b->n_scans < 0 || b->n_chunks < 0 || b->n_points < 0) return set_err(LSLAM_ERR_ARG, "negative sizes");
     if (b->n_scans == 0) return LSLAM_OK;
     if (!b->scan_chunk_off || !b->chunk_pt_off) return set_err(LSLAM_ERR_ARG, "missing CSR offsets");
-    if (need_points && !b->xy && b->n_points > 0) return set_err(LSLAM_ERR_ARG, "missing xy");
+    if (need_points && !b->xy && (!b->theta_deg || !b->dist_mm) && b->n_points > 0)
+        return set_err(LSLAM_ERR_ARG, "missing points (xy, or theta_deg + dist_mm)");
     if (b->max_chunk_points < 0 || b->max_scan_chunks < 0) return set_err(LSLAM_ERR_ARG, "bad maxima");
     return LSLAM_OK;
 }

@@ -33,14 +33,26 @@ class ScanPipeline:
     """Device-resident batch.  Build once, ``run()`` many times.
 
     Inputs are host numpy arrays (uploaded once).  Outputs are kept on the
-    device until ``results()`` downloads them.
+    device until ``results()`` downloads them.  Points are ``xy`` [P, 2], or
+    ``xy=None`` with the raw measures ``theta_deg`` / ``dist_mm`` [P]: then
+    functions.py:59-60 runs inside every kernel's point load (A1 fused).
     """
 
     def __init__(self, ctx: Context, xy, scan_chunk_off, chunk_pt_off, *, seeds=None, mt_state=None,
                  threshold=20.0, max_trials=100, hyp="mt19937", philox_seed=0x5EED5EED, hyp_draws=None,
                  landmarks=None, lmk_count=None, lmk_capacity=None, id_base=None,
-                 ukf=None, want_draws=False, want_counts=False, want_yproj=True, want_state=False):
+                 ukf=None, want_draws=False, want_counts=False, want_yproj=True, want_state=False,
+                 theta_deg=None, dist_mm=None):
         self.ctx = ctx
+        polar = xy is None
+        if polar:
+            if theta_deg is None or dist_mm is None:
+                raise ValueError("points: xy, or theta_deg and dist_mm")
+            theta_deg = np.ascontiguousarray(theta_deg, np.float64).ravel()
+            dist_mm = np.ascontiguousarray(dist_mm, np.float64).ravel()
+            if theta_deg.shape != dist_mm.shape:
+                raise ValueError("theta_deg / dist_mm size mismatch")
+            xy = np.zeros((theta_deg.size, 2))  # shape only
         dev_xy = xy if isinstance(xy, DeviceArray) else None  # e.g. ExpressRevolutions.xy: stays on the device
         if dev_xy is None:
             xy = np.ascontiguousarray(xy, np.float64).reshape(-1, 2)
@@ -63,7 +75,10 @@ class ScanPipeline:
         b.n_scans, b.n_chunks, b.n_points = S, Cn, P
         b.max_chunk_points = int(sizes.max()) if Cn else 0
         b.max_scan_chunks = int(per_scan.max()) if S else 0
-        if dev_xy is not None:
+        if polar:
+            b.theta_deg = d(theta_deg[:P] if P else np.zeros(1))
+            b.dist_mm = d(dist_mm[:P] if P else np.zeros(1))
+        elif dev_xy is not None:
             self._keep.append(dev_xy)
             b.xy = dev_xy.addr
         else:

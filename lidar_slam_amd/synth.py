@@ -131,22 +131,27 @@ def make_batch(scan_ids, n_beams: int = 720, cfg: int = 0):
     """Cartesian batch in the drop-in layout.
 
     Returns dict with ``xy`` (P,2) f64 (AoS, points of dropped remainders
-    excluded), ``scan_chunk_off`` (S+1) i32, ``chunk_pt_off`` (C+1) i32,
+    excluded), the raw measures ``theta_deg`` / ``dist_mm`` (P,),
+    ``scan_chunk_off`` (S+1) i32, ``chunk_pt_off`` (C+1) i32,
     ``poses`` (S,3).
     """
-    xs, poses, sco, cpo = [], [], [0], [0]
+    xs, ths, ds, poses, sco, cpo = [], [], [], [], [0], [0]
     for s in scan_ids:
         th, d, pose = scan_polar(s, n_beams, cfg)
         xy = polar_to_xy_ref(th, d)
         sizes = chunk_sizes(n_beams)
         used = int(sum(sizes))
         xs.append(xy[:used])
+        ths.append(th[:used])
+        ds.append(d[:used])
         for n in sizes:
             cpo.append(cpo[-1] + n)
         sco.append(sco[-1] + len(sizes))
         poses.append(pose)
     return {
         "xy": np.ascontiguousarray(np.concatenate(xs, axis=0)),
+        "theta_deg": np.concatenate(ths),
+        "dist_mm": np.concatenate(ds),
         "scan_chunk_off": np.asarray(sco, dtype=np.int32),
         "chunk_pt_off": np.asarray(cpo, dtype=np.int32),
         "poses": np.asarray(poses),
