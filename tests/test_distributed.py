@@ -7,7 +7,6 @@ import os
 import socket
 
 import numpy as np
-import pytest
 import torch.multiprocessing as mp
 
 

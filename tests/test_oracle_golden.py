@@ -8,7 +8,6 @@ landmark ids/lives and list evolution.  Within tolerance: the final direction
 (a, b, tip y, projected y).
 """
 import numpy as np
-import pytest
 
 from oracle import cpu as orc
 
