@@ -1735,6 +1735,12 @@ struct lslam_ctx {
     hipEvent_t ev_slot_free[2];  // on stream, after the slot's resolve + fix-up
     hipEvent_t ev_produced;      // on pstream, after rng_kernel
     hipEvent_t ev_copy;          // on stream, after the latest lslam_h2d / lslam_memset
+    // destinations written by copies since the producer last waited for ev_copy: the producer
+    // waits only if one of them is its input (seeds, CSR, MT state), so an xy upload per call
+    // overlaps the stream parse
+    struct { const void *p; size_t n; } copy_rng[32];
+    int n_copy_rng;
+    int copy_unknown;
     hipEvent_t ev_call;          // on stream, at the end of the latest pipeline call
     // A UKF step that does not read the call's RANSAC results runs on its own
     // stream beside the RANSAC chain; the main stream joins it before ev_call.
@@ -1929,6 +1935,19 @@ int lslam_host_free(void *p) {
     return LSLAM_OK;
 }
 
+static void note_copy(lslam_ctx *c, const void *p, size_t n) {
+    if (!p || !n) return;
+    for (int i = 0; i < c->n_copy_rng; i++)
+        if (c->copy_rng[i].p == p && c->copy_rng[i].n == n) return;
+    if (c->n_copy_rng == 32) {
+        c->copy_unknown = 1;
+        return;
+    }
+    c->copy_rng[c->n_copy_rng].p = p;
+    c->copy_rng[c->n_copy_rng].n = n;
+    c->n_copy_rng++;
+}
+
 int lslam_h2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
     if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
     if (!n) return LSLAM_OK;
@@ -1936,6 +1955,7 @@ int lslam_h2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    note_copy(c, dst, n);
     return LSLAM_OK;
 }
 
@@ -1956,6 +1976,7 @@ int lslam_memset(lslam_ctx *c, void *dst, int v, size_t n) {
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
     HIPCHK(hipMemsetAsync(dst, v, n, c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    note_copy(c, dst, n);
     return LSLAM_OK;
 }
 
@@ -2420,6 +2441,18 @@ static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
     return x < y + nb && y < x + na;
 }
 
+// did a copy since the producer last synchronised with ev_copy write one of its inputs?
+static bool copy_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
+    if (c->copy_unknown) return true;
+    const void *in[4] = {b->seeds, b->scan_chunk_off, b->chunk_pt_off, b->mt_state_in};
+    const size_t len[4] = {(size_t)b->n_scans * 4, (size_t)(b->n_scans + 1) * 4, (size_t)(b->n_chunks + 1) * 4,
+                           (size_t)b->n_scans * 625 * 4};
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < c->n_copy_rng; j++)
+            if (ranges_overlap(in[i], len[i], c->copy_rng[j].p, c->copy_rng[j].n)) return true;
+    return false;
+}
+
 // does the producer of this call read anything the previous pipeline call wrote?
 // 0: no; 1: only the previous call's mt_state_out (final once that call's fix-up ran:
 // a chained stream, e.g. LandmarkMap steps); 2: something else (wait for the whole call)
@@ -2636,7 +2669,11 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         // producer on its own stream: it waits for its slot's previous consumers, for input
         // copies, and (on a hazard) for the previous call; the consumers wait for it
         HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
-        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
+        if (copy_hazard(c, b)) {
+            HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
+            c->n_copy_rng = 0;
+            c->copy_unknown = 0;
+        }
         const int hz = producer_hazard(c, b);
         if (hz == 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
         if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
@@ -2856,6 +2893,10 @@ int lslam_express_scans(lslam_ctx *c, const uint8_t *packets, int64_t n_packets,
     if ((st = timer_end(c, LSLAM_K_EXPRESS))) return st;
     // the outputs may feed a pipeline call whose MT producer runs on the other stream
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    note_copy(c, out->xy, (size_t)out->cap_points * 16);
+    note_copy(c, out->scan_chunk_off, ((size_t)out->cap_scans + 1) * 4);
+    note_copy(c, out->chunk_pt_off, ((size_t)out->cap_chunks + 1) * 4);
+    note_copy(c, out->counts, 16);
     return LSLAM_OK;
 }
 
