@@ -63,7 +63,16 @@ def main(tag):
     for k, v in per.items():
         lines.append("- `%s`: FETCH_SIZE %.1f KiB, WRITE_SIZE %.1f KiB -> %d bytes/launch"
                      % (k, v["fetch_kib"], v["write_kib"], v["bytes_per_launch"]))
-    lines += ["", "bench.py line of the same build:", "", "```", json.dumps(bench), "```"]
+    # the profiled process's own bench line: its HIP-event kernel time must agree with rocprof's
+    prof_line = [l for l in open(os.path.join(OUT, "prof_kt.log")) if l.startswith('{"metric"')]
+    if prof_line:
+        pb = json.loads(prof_line[-1])
+        roc = [float(r["AverageNs"]) / 1e3 for r in stats if "rng_kernel" in r["Name"]]
+        lines += ["", "Dominant kernel, the profiled run itself: bench.py HIP events %.1f us per launch "
+                  "(rng_kernel), rocprofv3 average %.1f us (%+.1f %%); step %.4f ms under the profiler."
+                  % (1e3 * pb["roofline"]["kernel_ms"], roc[0] if roc else float("nan"),
+                     100.0 * ((roc[0] if roc else 0) / (1e3 * pb["roofline"]["kernel_ms"]) - 1.0), pb["ms_per_step"])]
+    lines += ["", "bench.py line of the same build (separate run, no profiler):", "", "```", json.dumps(bench), "```"]
     open(os.path.join(PROF, "%s_rocprof.md" % tag), "w").write("\n".join(lines) + "\n")
     for src in ("prof_kt/kt_kernel_stats.csv",):
         data = open(os.path.join(OUT, src)).read()
