@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSLAM_LIB") or os.path.join(_HERE, "liblidarslam.so")  # override: experiments
 
 # ---- constants mirrored from include/lidarslam.h ----
+ABI_VERSION = 2  # include/lidarslam.h LSLAM_ABI_VERSION (struct layouts below)
 LSLAM_OK = 0
 LSLAM_ERR_ARG = -1
 LSLAM_ERR_HIP = -2

@@ -1774,7 +1774,9 @@ static int set_err(int code, const char *msg) {
 
 extern "C" {
 
-const char *lslam_version(void) { return "lidarslam-mi355x 0.1.0 (abi 1, gfx950)"; }
+#define LSLAM_STR_(x) #x
+#define LSLAM_STR(x) LSLAM_STR_(x)
+const char *lslam_version(void) { return "lidarslam-mi355x 0.1.0 (abi " LSLAM_STR(LSLAM_ABI_VERSION) ", gfx950)"; }
 
 const char *lslam_status_string(int st) {
     switch (st) {

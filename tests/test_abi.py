@@ -41,6 +41,7 @@ def test_struct_layouts():
 def test_version_and_defaults():
     L = _lib.load()
     assert b"gfx950" in L.lslam_version()
+    assert b"(abi %d," % _lib.ABI_VERSION in L.lslam_version()
     p = _lib.ransac_params()
     assert (p.residual_threshold, p.max_trials, p.min_samples, p.life) == (20.0, 100, 2, 40)
     assert (p.tol_a, p.tol_b, p.tol_dist) == (0.1, 10.0, 100.0)
