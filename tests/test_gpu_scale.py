@@ -69,14 +69,35 @@ def test_c3_full_batch_properties(ctx):
 
 
 def test_c4_shard_8192(ctx):
+    """Rank 1's shard of C4 (65,536 scans over 8 GPUs, `bench.py --gpus 8 --scans 8192`) equals
+    the same scans run as two 4096-scan launches (ranks 2 and 3 of the default bench), and the
+    oracle on a sample."""
     import bench
-    ids = list(range(8192, 16384))   # rank 1's shard of 65,536 over 8 GPUs (2 x 4096 per bench rank)
+    from oracle import cpu as orc
+    ids = list(range(8192, 16384))
     b, ukf = bench.make_workload(ids, 720, 20, seed_base=1)
     r = _run(ctx, b, ids, ukf)
     m = r["models"]
+    cpo = b["chunk_pt_off"]
     assert np.all(m["flags"] & 1)
-    pop = np.add.reduceat(r["mask"].astype(np.int64), b["chunk_pt_off"][:-1])
+    pop = np.add.reduceat(r["mask"].astype(np.int64), cpo[:-1])
     assert np.array_equal(pop, m["n_inliers"])
+    for lo, hi in ((0, 4096), (4096, 8192)):
+        c0, c1 = b["scan_chunk_off"][lo], b["scan_chunk_off"][hi]
+        bb = {"xy": b["xy"][cpo[c0]:cpo[c1]], "scan_chunk_off": b["scan_chunk_off"][lo:hi + 1] - c0,
+              "chunk_pt_off": cpo[c0:c1 + 1] - cpo[c0]}
+        uk = {k: (v[lo:hi] if isinstance(v, np.ndarray) and v.shape[:1] == (8192,) else v) for k, v in ukf.items()}
+        rs = _run(ctx, bb, ids[lo:hi], uk)
+        assert np.array_equal(rs["mask"], r["mask"][cpo[c0]:cpo[c1]])
+        assert rs["models"].tobytes() == m[c0:c1].tobytes()
+        for k in ("mt_state", "landmarks", "lmk_count", "ukf_x", "ukf_P"):
+            assert np.array_equal(rs[k], r[k][lo:hi]), k
+    for i in np.random.default_rng(4).choice(8192, 8, replace=False):
+        c0, c1 = b["scan_chunk_off"][i], b["scan_chunk_off"][i + 1]
+        mask, _, models, lists = orc.run_batch(b["xy"][cpo[c0]:cpo[c1]], np.array([0, c1 - c0]),
+                                               cpo[c0:c1 + 1] - cpo[c0], [ids[i]])
+        assert np.array_equal(mask, r["mask"][cpo[c0]:cpo[c1]]), i
+        assert [L["id"] for L in lists[0]] == list(r["landmarks"][i, :r["lmk_count"][i]]["id"]), i
 
 
 def test_c5_dense_scans_and_l200_ukf(ctx):
