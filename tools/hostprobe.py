@@ -2,7 +2,8 @@
 call that blocks for about a step's length means the host, not the GPU, paces
 the stream of calls.
 
-python tools/hostprobe.py
+python tools/hostprobe.py [--no-timing]   (--no-timing: only the pass without HIP-event timers,
+                                          e.g. under rocprofv3 --kernel-trace for a timeline)
 """
 import os
 import sys
@@ -20,7 +21,7 @@ ids = list(range(4096))
 b, ukf = make_workload(ids, 720, 20)
 p = pl.ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids), lmk_capacity=32,
                     ukf=ukf)
-for timing in (False, True):
+for timing in ((False,) if "--no-timing" in sys.argv else (False, True)):
     ctx.set_timing(timing)
     for _ in range(3):
         p.run(sync=False)
