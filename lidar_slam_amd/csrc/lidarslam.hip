@@ -332,10 +332,10 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
     o.n_inl = 0;
     o.last_inl = -1;
     o.n_draws = T + 1;
-    // Reassociated cross product r = fl(fl(x uy - y ux) - k), k = ox uy - oy ux
-    // per hypothesis, with the band widened by the R sqrt(ecut) term (see
-    // count_kernel) and tested as two cutoffs on |r|: 3 FP64 ops + S + two
-    // counts per evaluation.  A lane whose counts differ (a point in the band)
+    // Reassociated cross product r = fl(x uy - fl(y ux + k)) (two fmas),
+    // k = ox uy - oy ux per hypothesis, with the band widened by the
+    // R sqrt(ecut) term (see count_kernel) and tested as two cutoffs on |r|:
+    // 2 FP64 ops + S + two counts per evaluation.  A lane whose counts differ (a point in the band)
     // or whose direction is not unit recounts exactly.
     const double Rb = unid(fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx)));
     const double margin = (E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
@@ -353,8 +353,8 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         int p = 0;
         for (; p + 2 <= N; p += 2) {
             const double2 q0 = P[p], q1 = P[p + 1];
-            const double r0 = __builtin_fma(q0.x, m.uy, -(q0.y * m.ux)) - k;
-            const double r1 = __builtin_fma(q1.x, m.uy, -(q1.y * m.ux)) - k;
+            const double r0 = __builtin_fma(q0.x, m.uy, -__builtin_fma(q0.y, m.ux, k));
+            const double r1 = __builtin_fma(q1.x, m.uy, -__builtin_fma(q1.y, m.ux, k));
             S = __builtin_fma(r0, r0, S);
             S = __builtin_fma(r1, r1, S);
             lo += (int)(fabs(r0) <= r_lo) + (int)(fabs(r1) <= r_lo);
@@ -362,7 +362,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         }
         if (p < N) {
             const double2 q = P[p];
-            const double r = __builtin_fma(q.x, m.uy, -(q.y * m.ux)) - k;
+            const double r = __builtin_fma(q.x, m.uy, -__builtin_fma(q.y, m.ux, k));
             S = __builtin_fma(r, r, S);
             lo += (int)(fabs(r) <= r_lo);
             hi += (int)(fabs(r) < r_hi);
@@ -371,7 +371,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         if (exact_all || lo != hi) {  // rare: lane-divergent exact recount
             c = 0;
             for (int q = 0; q < N; q++) {
-                const double r = __builtin_fma(P[q].x, m.uy, -(P[q].y * m.ux)) - k;
+                const double r = __builtin_fma(P[q].x, m.uy, -__builtin_fma(P[q].y, m.ux, k));
                 const double v = r * r;
                 bool in = v < ecut;
                 if (exact_all || fabs(v - ecut) <= margin) in = resid2(P[q], m) < ecut;
@@ -1393,12 +1393,14 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     const ChunkBox bx = box_finish(xmn, xmx, ymn, ymx, s_fin[0] && s_fin[1] && s_fin[2] && s_fin[3]);
     const double ecut = a.ecut;
     const bool cheap = bx.finite && ecut < __builtin_inf();
-    // The main loop evaluates the cross product as r = fl(fl(x uy - y ux) - k),
-    // k = fl(ox uy - oy ux) per hypothesis: 3 FP64 ops instead of 4.  Against
-    // chunk_consensus's fl(ex uy - ey ux) this adds at most ~8 u R |r| to r^2
-    // (R = max|x| + max|y| over the chunk box, which holds o), so the band
-    // gets an R sqrt(ecut) term; 2^-42 leaves a factor 2^8 of slack on it as on
-    // the E2 term.  Outside the band the cheap test decides as before.
+    // The main loop evaluates the cross product as r = fl(x uy - fl(y ux + k))
+    // (two fmas), k = fl(ox uy - oy ux) per hypothesis: 2 FP64 ops instead of 4.
+    // |y ux + k| <= 2R, so the inner rounding is <= 2uR, the outer <= u|r| and
+    // k's own <= 2uR: against the direct fl(ex uy - ey ux) this adds at most
+    // ~8 u R |r| to r^2 (R = max|x| + max|y| over the chunk box, which holds
+    // o), so the band gets an R sqrt(ecut) term; 2^-42 leaves a factor 2^8 of
+    // slack on it as on the E2 term.  Outside the band the cheap test decides
+    // as before.
     const double Rb = fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx));
     const double margin = (bx.E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
     // c2 < ecut - margin  <=>  |r| <= r_lo;   c2 > ecut + margin  <=>  |r| >= r_hi
@@ -1426,7 +1428,7 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
                 uint32_t nlo = 0, nhi = 0;
 #pragma unroll
                 for (int j = 0; j < PPL; j++) {
-                    const double r = __builtin_fma(qx[j], uy, -(qy[j] * ux)) - k;
+                    const double r = __builtin_fma(qx[j], uy, -__builtin_fma(qy[j], ux, k));
                     nlo += (uint32_t)popc64(ballot(fabs(r) <= r_lo));
                     nhi += (uint32_t)popc64(ballot(fabs(r) < r_hi));
                 }
