@@ -24,7 +24,9 @@ import os
 import sys
 import time
 
-import numpy as np
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # the CPU baseline's twin is single-threaded per process
+
+import numpy as np  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -56,7 +58,6 @@ def mt_stream_ops(chunk_sizes, trials):
 
 def make_workload(scan_ids, n_beams, L, seed_base=0):
     from lidar_slam_amd import synth
-    from oracle import ukf as oukf  # noqa: F401  (only for the data generator's hx below)
     b = synth.make_batch(scan_ids, n_beams)
     S = len(scan_ids)
     rng = np.random.default_rng(424242 + seed_base)
@@ -84,10 +85,7 @@ def _twin_worker(args):
     return 1
 
 
-def cpu_baseline(n_scans, n_beams, L, procs):
-    """The reference's CPU path (NumPy twin, per-trial skimage structure) +
-    the NumPy UKF restatement, over a bounded sample, on `procs` host cores."""
-    import multiprocessing as mp
+def _twin_jobs(n_scans, n_beams, L):
     ids = list(range(n_scans))
     b, ukf = make_workload(ids, n_beams, L)
     sco, cpo = b["scan_chunk_off"], b["chunk_pt_off"]
@@ -96,6 +94,44 @@ def cpu_baseline(n_scans, n_beams, L, procs):
         c0, c1 = sco[s], sco[s + 1]
         jobs.append((b["xy"][cpo[c0]:cpo[c1]], cpo[c0:c1 + 1] - cpo[c0], s,
                      (ukf["x"][s], ukf["P"][s], ukf["u"][s], ukf["z"][s], ukf["lmk"][s], ukf["R_diag"])))
+    return jobs
+
+
+def cpu_baseline_1core(n_scans, n_beams, L):
+    """The same twin in this process alone: one core (OPENBLAS_NUM_THREADS=1 is set at import)."""
+    jobs = _twin_jobs(n_scans, n_beams, L)
+    _twin_worker(jobs[0])
+    t0 = time.perf_counter()
+    for j in jobs:
+        _twin_worker(j)
+    dt = time.perf_counter() - t0
+    return len(jobs) / dt, dt
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def capacity_overflows(models):
+    """Chunks whose new landmark was dropped because the per-scan list was full (LSLAM_CAPACITY).
+    The reference's list is unbounded (ransac_functions.py:75-76): a timed step is
+    reference-exact only if this is 0."""
+    return int(np.sum((models["flags"] & 256) != 0))
+
+
+def cpu_baseline(n_scans, n_beams, L, procs):
+    """The reference's CPU path (NumPy twin, per-trial skimage structure) +
+    the NumPy UKF restatement, over a bounded sample, on `procs` host cores."""
+    import multiprocessing as mp
+    jobs = _twin_jobs(n_scans, n_beams, L)
     ctx = mp.get_context("fork")
     with ctx.Pool(procs) as pool:
         pool.map(_twin_worker, jobs[:procs])  # warm the workers (imports)
@@ -155,7 +191,10 @@ def main():
     ap.add_argument("--no-ukf", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1024)
+    ap.add_argument("--cpu-sample-1core", type=int, default=96)
     ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--lmk-capacity", type=int, default=64,
+                    help="per-scan landmark list capacity (>= the steady-state list, ~42 on C3)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     ap.add_argument("--also-philox", action="store_true", help="also time the Philox (throughput) mode")
     args = ap.parse_args()
@@ -169,12 +208,15 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         procs = args.cpu_procs or max(1, min(16, os.cpu_count() or 1))
+        rate1, dt1 = cpu_baseline_1core(args.cpu_sample_1core, args.beams, L)
         rate, dt = cpu_baseline(args.cpu_sample, args.beams, L, procs)
         cpu = {"value": round(rate, 2), "unit": "scans/s", "cores": procs, "kind": "port",
+               "value_1core": round(rate1, 2), "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
                "sample": "%d synthetic %d-pt scans (same generator, per-scan seeds) through the NumPy twin of "
                          "the reference (skimage-structured ransac + landmark association, oracle/numpy_twin.py) "
-                         "+ the NumPy UKF restatement (oracle/ukf.py), %d processes, %.1f s wall"
-                         % (args.cpu_sample, args.beams, procs, dt)}
+                         "+ the NumPy UKF restatement (oracle/ukf.py), %d processes, %.1f s wall; 1 core: %d "
+                         "scans in %.1f s; twin/reference calibration in BASELINE.md"
+                         % (args.cpu_sample, args.beams, procs, dt, args.cpu_sample_1core, dt1)}
 
     dist = None
     if world > 1:
@@ -190,7 +232,7 @@ def main():
     ids = shard_scan_ids(rank, S)
     b, ukf = make_workload(ids, args.beams, L, seed_base=rank)
     pipe = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
-                        max_trials=args.trials, hyp=args.hyp, lmk_capacity=32, want_yproj=True,
+                        max_trials=args.trials, hyp=args.hyp, lmk_capacity=args.lmk_capacity, want_yproj=True,
                         ukf=None if args.no_ukf else ukf)
     try:
         import torch
@@ -231,6 +273,7 @@ def main():
     # sanity: results are well-formed (every chunk fitted or flagged)
     r = pipe.results()
     valid = int(np.sum((r["models"]["flags"] & 1) != 0))
+    overflows = capacity_overflows(r["models"])  # of the last timed step (the lists chain across steps)
 
     total_scans = S * world * args.steps
     value = total_scans / elapsed
@@ -299,10 +342,12 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "valid_chunks": valid,
+        "capacity_overflows": overflows,
+        "max_landmark_list": int(np.max(r["lmk_count"])),
     }
     if args.also_philox and world == 1:
         pipe2 = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], max_trials=args.trials,
-                             hyp="philox", lmk_capacity=32, ukf=None if args.no_ukf else ukf)
+                             hyp="philox", lmk_capacity=args.lmk_capacity, ukf=None if args.no_ukf else ukf)
         for _ in range(args.warmup):
             pipe2.run(sync=False)
         ctx.sync()
@@ -315,6 +360,9 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if overflows:
+        sys.exit("capacity_overflows = %d: raise --lmk-capacity (the timed step was not reference-exact)"
+                 % overflows)
 
 
 if __name__ == "__main__":

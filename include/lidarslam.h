@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LSLAM_ABI_VERSION 2
+#define LSLAM_ABI_VERSION 3
 
 /* ---- status codes ---- */
 enum {
@@ -228,7 +228,22 @@ int lslam_host_alloc(size_t bytes, void **hptr);  /* pinned host memory */
 int lslam_host_free(void *hptr);
 int lslam_h2d(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
 int lslam_d2h(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
+int lslam_d2d(lslam_ctx *ctx, void *dst, const void *src, size_t bytes);  /* async */
 int lslam_memset(lslam_ctx *ctx, void *dst, int value, size_t bytes);     /* async */
+/* Page-lock existing host memory (hipHostRegister), e.g. a host batch shared between the
+ * ranks of one node (the reference's mp.Queue hand-off, SLAM.py:13,18-23, done as shared
+ * memory + per-rank H2D of a shard): lslam_h2d / lslam_d2h from it then run at PCIe rate. */
+int lslam_host_register(void *hptr, size_t bytes);
+int lslam_host_unregister(void *hptr);
+/* The context's main HIP stream (a hipStream_t).  Work a caller enqueues on it, e.g. an RCCL
+ * gather of a pipeline call's outputs (lidar_slam_amd/collective.py), runs after every call made
+ * on the context so far and before later ones.  It must not write a buffer a later call's MT
+ * producer reads (seeds, CSR offsets, mt_state_in) unless followed by lslam_sync. */
+int lslam_ctx_stream(lslam_ctx *ctx, void **stream);
+/* sizes (bytes) of the ABI structs as compiled into the library, in this order:
+ * lslam_chunk_model, lslam_landmark, lslam_ransac_params, lslam_ukf_params, lslam_scan_batch,
+ * lslam_express_measures, lslam_express_revs.  Writes min(n, 7) entries, returns 7. */
+int lslam_abi_sizes(int64_t *sizes, int n);
 /* per-kernel HIP-event timing on the ctx stream (kernel ids: LSLAM_K_*) */
 enum { LSLAM_K_POLAR = 0, LSLAM_K_HYP = 1, LSLAM_K_PIPELINE = 2, LSLAM_K_LANDMARK = 3, LSLAM_K_UKF = 4,
        LSLAM_K_RNG = 5 /* parity-stream producer */, LSLAM_K_CONSENSUS = 6 /* per-chunk A4-A8 */,

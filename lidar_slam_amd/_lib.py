@@ -8,12 +8,13 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSLAM_LIB") or os.path.join(_HERE, "liblidarslam.so")  # override: experiments
 
 # ---- constants mirrored from include/lidarslam.h ----
-ABI_VERSION = 2  # include/lidarslam.h LSLAM_ABI_VERSION (struct layouts below)
+ABI_VERSION = 3  # include/lidarslam.h LSLAM_ABI_VERSION (struct layouts below)
 LSLAM_OK = 0
 LSLAM_ERR_ARG = -1
 LSLAM_ERR_HIP = -2
@@ -87,7 +88,8 @@ assert C.sizeof(LandmarkRec) == 56
 EXPORTS = [
     "lslam_version", "lslam_status_string", "lslam_last_error", "lslam_device_count", "lslam_ctx_create",
     "lslam_ctx_destroy", "lslam_sync", "lslam_malloc", "lslam_free", "lslam_host_alloc", "lslam_host_free",
-    "lslam_h2d", "lslam_d2h", "lslam_memset", "lslam_set_timing", "lslam_set_timing_mask", "lslam_timing",
+    "lslam_h2d", "lslam_d2h", "lslam_d2d", "lslam_memset", "lslam_host_register", "lslam_host_unregister",
+    "lslam_ctx_stream", "lslam_abi_sizes", "lslam_set_timing", "lslam_set_timing_mask", "lslam_timing",
     "lslam_timing_reset",
     "lslam_ransac_params_default", "lslam_ukf_params_default", "lslam_inlier_cutoff", "lslam_ukf_weights",
     "lslam_mt_seed_state", "lslam_polar_to_xy", "lslam_hyp_mt19937", "lslam_ransac", "lslam_landmarks",
@@ -130,7 +132,12 @@ def load():
         "lslam_host_free": ([_VP], C.c_int),
         "lslam_h2d": ([_VP, _VP, _VP, sz], C.c_int),
         "lslam_d2h": ([_VP, _VP, _VP, sz], C.c_int),
+        "lslam_d2d": ([_VP, _VP, _VP, sz], C.c_int),
         "lslam_memset": ([_VP, _VP, C.c_int, sz], C.c_int),
+        "lslam_host_register": ([_VP, sz], C.c_int),
+        "lslam_host_unregister": ([_VP], C.c_int),
+        "lslam_ctx_stream": ([_VP, P(_VP)], C.c_int),
+        "lslam_abi_sizes": ([P(i64), C.c_int], C.c_int),
         "lslam_set_timing": ([_VP, C.c_int], C.c_int),
         "lslam_set_timing_mask": ([_VP, u32], C.c_int),
         "lslam_timing": ([_VP, C.c_int, P(dbl), P(i64)], C.c_int),
@@ -149,12 +156,38 @@ def load():
         "lslam_express_decode": ([_VP, _VP, i64, P(ExpressMeasures)], C.c_int),
         "lslam_express_scans": ([_VP, _VP, i64, i32, P(ExpressRevs)], C.c_int),
     }
-    for name, (args, res) in sig.items():
-        f = getattr(L, name)
-        f.argtypes = args
-        f.restype = res
+    try:
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+    except AttributeError as e:
+        _err = HIPLibraryError("%s lacks %s: a stale build? rebuild with `python -m lidar_slam_amd.build`"
+                               % (LIB_PATH, e))
+        raise _err
+    _check_abi(L)
     _lib = L
     return L
+
+
+def _check_abi(L):
+    """The library must be the ABI these ctypes layouts describe: a stale .so (e.g. via LSLAM_LIB)
+    would silently ignore appended struct fields."""
+    global _err
+    ver = L.lslam_version().decode(errors="replace")
+    m = re.search(r"\(abi (\d+),", ver)
+    if not m or int(m.group(1)) != ABI_VERSION:
+        _err = HIPLibraryError("%s reports %r; this binding needs ABI %d (rebuild the library)"
+                               % (LIB_PATH, ver, ABI_VERSION))
+        raise _err
+    got = (C.c_int64 * 7)()
+    L.lslam_abi_sizes(got, 7)
+    want = [C.sizeof(t) for t in (ChunkModel, LandmarkRec, RansacParams, UkfParams, ScanBatch, ExpressMeasures,
+                                  ExpressRevs)]
+    if list(got) != want:
+        _err = HIPLibraryError("struct sizes differ between %s %s and the ctypes layouts %s"
+                               % (LIB_PATH, list(got), want))
+        raise _err
 
 
 def check(status, what=""):

@@ -1702,6 +1702,7 @@ __global__ __launch_bounds__(256) void polar_kernel(const double *__restrict__ t
 // host side
 // ------------------------------------------------------------------------
 constexpr int LSLAM_EV_RING = 64;
+constexpr int LSLAM_MAX_OUTS = 48;
 
 struct lslam_ctx {
     int device;
@@ -1748,10 +1749,13 @@ struct lslam_ctx {
     // stream beside the RANSAC chain; the main stream joins it before ev_call.
     hipStream_t ustream;
     hipEvent_t ev_ukf;           // on ustream, after the side UKF
-    // buffers written by the latest pipeline call (producer inputs must not alias them)
-    const void *out_ptr[12];
-    size_t out_len[12];
+    // Every buffer written by a call since the producer last waited for ev_call: the union
+    // over calls, not only the latest (the producer of call k may start once call k-2's
+    // fix-up has run).  A producer input that overlaps one of them makes it wait.
+    const void *out_ptr[LSLAM_MAX_OUTS];
+    size_t out_len[LSLAM_MAX_OUTS];
     int n_out;
+    int out_unknown;             // the union overflowed: the producer waits for ev_call
     // the latest call's mt_state_out, complete once ev_slot_free[prev_slot] (after its fix-up) fired
     const void *prev_state_out;
     int prev_slot;
@@ -1778,7 +1782,7 @@ extern "C" {
 
 #define LSLAM_STR_(x) #x
 #define LSLAM_STR(x) LSLAM_STR_(x)
-const char *lslam_version(void) { return "lidarslam-mi355x 0.1.0 (abi " LSLAM_STR(LSLAM_ABI_VERSION) ", gfx950)"; }
+const char *lslam_version(void) { return "lidarslam-mi355x 0.2.0 (abi " LSLAM_STR(LSLAM_ABI_VERSION) ", gfx950)"; }
 
 const char *lslam_status_string(int st) {
     switch (st) {
@@ -1971,6 +1975,44 @@ int lslam_d2h(lslam_ctx *c, void *dst, const void *src, size_t n) {
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
     return LSLAM_OK;
+}
+
+int lslam_d2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
+    if (!n) return LSLAM_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->ev_copy, c->stream));
+    note_copy(c, dst, n);
+    return LSLAM_OK;
+}
+
+int lslam_host_register(void *p, size_t n) {
+    if (!p || !n) return LSLAM_ERR_ARG;
+    HIPCHK(hipHostRegister(p, n, hipHostRegisterDefault));
+    return LSLAM_OK;
+}
+
+int lslam_host_unregister(void *p) {
+    if (!p) return LSLAM_ERR_ARG;
+    HIPCHK(hipHostUnregister(p));
+    return LSLAM_OK;
+}
+
+int lslam_ctx_stream(lslam_ctx *c, void **stream) {
+    if (!c || !stream) return LSLAM_ERR_ARG;
+    *stream = (void *)c->stream;
+    return LSLAM_OK;
+}
+
+int lslam_abi_sizes(int64_t *sizes, int n) {
+    const int64_t s[7] = {(int64_t)sizeof(lslam_chunk_model), (int64_t)sizeof(lslam_landmark),
+                          (int64_t)sizeof(lslam_ransac_params), (int64_t)sizeof(lslam_ukf_params),
+                          (int64_t)sizeof(lslam_scan_batch), (int64_t)sizeof(lslam_express_measures),
+                          (int64_t)sizeof(lslam_express_revs)};
+    for (int i = 0; i < n && i < 7 && sizes; i++) sizes[i] = s[i];
+    return 7;
 }
 
 int lslam_memset(lslam_ctx *c, void *dst, int v, size_t n) {
@@ -2461,6 +2503,7 @@ static bool copy_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
 // 0: no; 1: only the previous call's mt_state_out (final once that call's fix-up ran:
 // a chained stream, e.g. LandmarkMap steps); 2: something else (wait for the whole call)
 static int producer_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
+    if (c->out_unknown) return 2;
     const void *in[4] = {b->seeds, b->scan_chunk_off, b->chunk_pt_off, b->mt_state_in};
     const size_t len[4] = {(size_t)b->n_scans * 4, (size_t)(b->n_scans + 1) * 4, (size_t)(b->n_chunks + 1) * 4,
                            (size_t)b->n_scans * 625 * 4};
@@ -2472,20 +2515,35 @@ static int producer_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
     return level;
 }
 
+// add [p, p + n) to the union of buffers written since the producer last waited for ev_call
+static void note_out(lslam_ctx *c, const void *p, size_t n) {
+    if (!p || !n) return;
+    for (int i = 0; i < c->n_out; i++)
+        if (c->out_ptr[i] == p && c->out_len[i] == n) return;
+    if (c->n_out == LSLAM_MAX_OUTS) {
+        c->out_unknown = 1;
+        return;
+    }
+    c->out_ptr[c->n_out] = p;
+    c->out_len[c->n_out] = n;
+    c->n_out++;
+}
+
 static void remember_outputs(lslam_ctx *c, const lslam_scan_batch *b, int T, int L) {
     const size_t S = (size_t)b->n_scans, C = (size_t)b->n_chunks, P = (size_t)b->n_points;
-    const void *p[12] = {b->inlier_mask, b->models, b->y_proj, b->draws_out, b->trial_cnt_out, b->mt_state_out,
-                         b->landmarks, b->lmk_count, b->lmk_walk, b->ukf_x, b->ukf_P, nullptr};
-    const size_t n[12] = {P, C * sizeof(lslam_chunk_model), P * 8, C * 2 * (T + 1) * 4, C * T * 4, S * 625 * 4,
+    const void *p[11] = {b->inlier_mask, b->models, b->y_proj, b->draws_out, b->trial_cnt_out, b->mt_state_out,
+                         b->landmarks, b->lmk_count, b->lmk_walk, b->ukf_x, b->ukf_P};
+    const size_t n[11] = {P, C * sizeof(lslam_chunk_model), P * 8, C * 2 * (T + 1) * 4, C * T * 4, S * 625 * 4,
                           S * b->lmk_capacity * sizeof(lslam_landmark), S * 4, S * b->lmk_capacity * 4,
-                          L ? S * 24 : 0, L ? S * 72 : 0, 0};
-    c->n_out = 0;
-    for (int i = 0; i < 12; i++)
-        if (p[i] && n[i]) {
-            c->out_ptr[c->n_out] = p[i];
-            c->out_len[c->n_out] = n[i];
-            c->n_out++;
-        }
+                          L ? S * 24 : 0, L ? S * 72 : 0};
+    for (int i = 0; i < 11; i++) note_out(c, p[i], n[i]);
+}
+
+// every entry point that enqueues device work ends here: later calls order against ev_call
+// (h2d / d2h / memset, the side-stream UKF and, on a hazard, the next MT producer)
+static int end_call(lslam_ctx *c) {
+    HIPCHK(hipEventRecord(c->ev_call, c->stream));
+    return LSLAM_OK;
 }
 
 // select_kernel LDS: the chunk's points, tied trials, tie sums / inlier list, mask, sum scratch
@@ -2679,7 +2737,12 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
             c->copy_unknown = 0;
         }
         const int hz = producer_hazard(c, b);
-        if (hz == 2) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
+        if (hz == 2) {
+            // ev_call follows every call enqueued so far: the union starts afresh
+            HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
+            c->n_out = 0;
+            c->out_unknown = 0;
+        }
         if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
         KArgs kr = k;
         kr.b.mt_state_out = k.state_scr;
@@ -2715,7 +2778,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (st) return st;
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
-    HIPCHK(hipEventRecord(c->ev_call, c->stream));
+    if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_PIPELINE);
 }
 
@@ -2759,7 +2822,8 @@ int lslam_polar_to_xy(lslam_ctx *c, const double *th, const double *d, double *x
     HIPCHK(hipGetLastError());
     st = timer_end(c, LSLAM_K_POLAR);
     if (st) return st;
-    return LSLAM_OK;
+    note_out(c, xy, (size_t)n * 16);
+    return end_call(c);
 }
 
 int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trials) {
@@ -2789,6 +2853,14 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     st = launch_resolve(c, k);
     if (st) return st;
     HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+    // the end state is written by the rng kernel itself, final at ev_slot_free[slot]: a
+    // pipeline call chaining from it waits for that event, anything else for ev_call
+    note_out(c, b->draws_out, (size_t)b->n_chunks * 2 * (size_t)(max_trials + 1) * 4);
+    note_out(c, b->mt_state_out, (size_t)b->n_scans * 625 * 4);
+    c->prev_state_out = b->mt_state_out;
+    c->prev_slot = slot;
+    c->prev_fixed = b->mt_state_out ? 1 : 0;
+    if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_HYP);
 }
 
@@ -2808,7 +2880,9 @@ int lslam_landmarks(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_
     int lds = 0;
     st = build_args(k, b, p, nullptr, MODE_ASSOC, lds);
     if (st) return st;
-    return run_scan_kernel<MODE_ASSOC>(c, k, lds, LSLAM_K_LANDMARK);
+    if ((st = run_scan_kernel<MODE_ASSOC>(c, k, lds, LSLAM_K_LANDMARK))) return st;
+    remember_outputs(c, b, k.T, 0);
+    return end_call(c);
 }
 
 int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u) {
@@ -2821,7 +2895,10 @@ int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_para
     if (!bb.scan_chunk_off) return set_err(LSLAM_ERR_ARG, "scan_chunk_off required (may describe 0 chunks)");
     int st = build_args(k, &bb, nullptr, u, MODE_UKF, lds);
     if (st) return st;
-    return run_scan_kernel<MODE_UKF>(c, k, lds, LSLAM_K_UKF);
+    if ((st = run_scan_kernel<MODE_UKF>(c, k, lds, LSLAM_K_UKF))) return st;
+    note_out(c, b->ukf_x, (size_t)b->n_scans * 24);
+    note_out(c, b->ukf_P, (size_t)b->n_scans * 72);
+    return end_call(c);
 }
 
 int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p,
@@ -2843,7 +2920,15 @@ int lslam_express_decode(lslam_ctx *c, const uint8_t *packets, int64_t n_packets
     const int64_t blocks = (n_packets + EXP_DEC_PER_WG - 1) / EXP_DEC_PER_WG;
     hipLaunchKernelGGL(express_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, c->stream, packets, n_packets, o);
     HIPCHK(hipGetLastError());
-    return timer_end(c, LSLAM_K_EXPRESS);
+    if ((st = timer_end(c, LSLAM_K_EXPRESS))) return st;
+    const size_t nm = (size_t)(n_packets > 1 ? n_packets - 1 : 0) * 32;
+    note_out(c, out->angle_deg, nm * 8);
+    note_out(c, out->dist_mm, nm * 8);
+    note_out(c, out->new_scan, nm);
+    note_out(c, out->valid, nm);
+    note_out(c, out->xy, nm * 16);
+    note_out(c, out->pkt_valid, (size_t)n_packets);
+    return end_call(c);
 }
 
 int lslam_express_scans(lslam_ctx *c, const uint8_t *packets, int64_t n_packets, int32_t skip,
@@ -2901,7 +2986,7 @@ int lslam_express_scans(lslam_ctx *c, const uint8_t *packets, int64_t n_packets,
     note_copy(c, out->scan_chunk_off, ((size_t)out->cap_scans + 1) * 4);
     note_copy(c, out->chunk_pt_off, ((size_t)out->cap_chunks + 1) * 4);
     note_copy(c, out->counts, 16);
-    return LSLAM_OK;
+    return end_call(c);
 }
 
 }  // extern "C"

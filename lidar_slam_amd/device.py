@@ -46,6 +46,19 @@ class Context:
     def timing_reset(self):
         _lib.check(self._L.lslam_timing_reset(self.handle), "lslam_timing_reset")
 
+    @property
+    def stream(self):
+        """The context's main hipStream_t (int address), for collectives enqueued after its calls."""
+        s = C.c_void_p()
+        _lib.check(self._L.lslam_ctx_stream(self.handle, C.byref(s)), "lslam_ctx_stream")
+        return s.value or 0
+
+    def copy(self, dst, src, nbytes=None):
+        """Device-to-device copy on the context stream (async)."""
+        n = dst.nbytes if nbytes is None else int(nbytes)
+        _lib.check(self._L.lslam_d2d(self.handle, dst.ptr if isinstance(dst, DeviceArray) else C.c_void_p(dst),
+                                     src.ptr if isinstance(src, DeviceArray) else C.c_void_p(src), n), "lslam_d2d")
+
     def empty(self, shape, dtype):
         return DeviceArray(self, shape, dtype)
 
@@ -89,6 +102,16 @@ class DeviceArray:
                                          self.nbytes), "lslam_h2d")
         self.ctx.sync()  # arr may be a temporary: finish before it is freed
 
+    def upload_async(self, arr):
+        """H2D on the context stream without waiting: ``arr`` (ideally page-locked, see
+        ``register_host``) must stay alive and unchanged until the next ``ctx.sync()``."""
+        if not (isinstance(arr, np.ndarray) and arr.flags.c_contiguous and arr.dtype == self.dtype):
+            raise ValueError("upload_async needs a C-contiguous %s array" % self.dtype)
+        if arr.nbytes != self.nbytes:
+            raise ValueError("upload size mismatch %d != %d" % (arr.nbytes, self.nbytes))
+        _lib.check(self.ctx._L.lslam_h2d(self.ctx.handle, self.ptr, arr.ctypes.data_as(C.c_void_p),
+                                         self.nbytes), "lslam_h2d")
+
     def download(self, out=None):
         if out is None:
             out = np.empty(self.shape, self.dtype)
@@ -115,3 +138,12 @@ class DeviceArray:
 def ptr(x):
     """Device address of a DeviceArray (or None)."""
     return None if x is None else x.addr
+
+
+def register_host(arr) -> bool:
+    """Page-lock a host array in place (hipHostRegister); False if the runtime refuses."""
+    return _lib.load().lslam_host_register(arr.ctypes.data_as(C.c_void_p), arr.nbytes) == _lib.LSLAM_OK
+
+
+def unregister_host(arr):
+    _lib.load().lslam_host_unregister(arr.ctypes.data_as(C.c_void_p))

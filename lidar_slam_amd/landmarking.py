@@ -1,8 +1,14 @@
-"""Drop-in for ``landmarking.py`` (the reference's Landmark value object).
+"""Drop-in for ``landmarking.py``: the Landmark value object callers hold.
 
-Same class, constants, method names and semantics as landmarking.py:1-82.  The
-association walk of the hot path runs on the GPU (lslam_landmarks / the fused
-scan kernel); these methods remain for callers that use a Landmark directly.
+The hot path never calls these methods (the association walk of
+ransac_functions.py:34-54 runs on the GPU, lslam_landmarks / the scan kernel's
+post pass); the class is here so that code holding the reference's Landmark
+objects (check_ransac's list, mainWindow's plots) keeps its attribute and method
+surface: a, b, id, life, pos, end, timesObserved, spec and the accessors of
+landmarking.py:12-64, with the association semantics of landmarking.py:48-77
+(life floored at 0, ``is_equal`` with the three tolerances).  The reference's
+``landmarks_track`` (landmarking.py:79-82) is not provided: it is never called
+and, comparing a bound method with 0, never removes anything.
 """
 from __future__ import annotations
 
@@ -14,23 +20,26 @@ TOLERANCE_B = 10   # landmarking.py:5
 TOLERANCE = 100    # landmarking.py:6
 
 
+def _gap(p, q):
+    """Euclidean distance as numpy's norm computes it for 2-vectors (the reference uses np.linalg.norm)."""
+    return np.linalg.norm(np.asarray(p, np.float64) - np.asarray(q, np.float64))
+
+
 class Landmark():
     spec = "line"
 
     def __init__(self, a, b, ID, x, y, tipX, tipY):
-        self.a = a
-        self.b = b
-        self.id = ID
+        self.a, self.b, self.id = a, b, ID
+        self.pos = np.array([x, y])        # the fitted origin (inlier centroid)
+        self.end = np.array([tipX, tipY])  # the last inlier's x on the fitted line
         self.life = LIFE
-        self.pos = np.array([x, y])
-        self.end = np.array([tipX, tipY])
         self.timesObserved = 0
 
     def __str__(self):
-        return ("Landmark ID: {}\n".format(self.id)
-                + "(x, y): ({}, {})\n".format(self.pos[0], self.pos[1])
-                + "equation: {} * x + {}\n".format(self.a, self.b))
+        x, y = self.pos
+        return "Landmark ID: {}\n(x, y): ({}, {})\nequation: {} * x + {}\n".format(self.id, x, y, self.a, self.b)
 
+    # accessors the reference's callers use
     def get_id(self):
         return self.id
 
@@ -52,37 +61,26 @@ class Landmark():
     def observed(self):
         self.timesObserved += 1
 
-    def decrease_life(self):
-        """landmarking.py:48-52: floor at 0; True once it reaches 0, else None."""
-        if self.life > 0:
-            self.life -= 1
-        if self.life == 0:
-            return True
-
     def reset_life(self):
         self.life = LIFE
 
-    def distance_end_origin(self, landmark):
-        return np.linalg.norm(self.end - landmark.get_pos())
+    def decrease_life(self):
+        """One unmatched association pass: life floors at 0; True once it is 0, else None
+        (the caller removes the landmark on True, ransac_functions.py:39-41)."""
+        if self.life > 0:
+            self.life -= 1
+        return True if self.life == 0 else None
 
-    def distance_origin_end(self, landmark):
-        return np.linalg.norm(self.pos - landmark.get_end())
+    def distance_end_origin(self, other):
+        return _gap(self.end, other.get_pos())
 
-    def is_equal(self, landmark):
-        """landmarking.py:66-77."""
-        distA = abs(self.a - landmark.get_a())
-        distB = abs(self.b - landmark.get_b())
-        dEO = self.distance_end_origin(landmark)
-        dOE = self.distance_origin_end(landmark)
-        if distA <= TOLERANCE_A and distB <= TOLERANCE_B:
-            return bool(dEO <= TOLERANCE or dOE <= TOLERANCE)
-        return False
+    def distance_origin_end(self, other):
+        return _gap(self.pos, other.get_end())
 
-
-def landmarks_track(landmarks):
-    """landmarking.py:79-82, kept with the reference's behaviour: it compares
-    the bound method ``get_life`` (not its value) with 0, so it never removes
-    anything."""
-    for landmark in landmarks:
-        if landmark.get_life == 0:  # noqa: reference bug reproduced on purpose
-            landmarks.remove(landmark)
+    def is_equal(self, other):
+        """Same line (slope within TOLERANCE_A, intercept within TOLERANCE_B) and the two
+        segments continue each other (one's end within TOLERANCE of the other's origin)."""
+        same_line = abs(self.a - other.get_a()) <= TOLERANCE_A and abs(self.b - other.get_b()) <= TOLERANCE_B
+        if not same_line:  # (NaN slopes of vertical fits never match)
+            return False
+        return bool(self.distance_end_origin(other) <= TOLERANCE or self.distance_origin_end(other) <= TOLERANCE)

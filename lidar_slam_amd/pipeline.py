@@ -87,7 +87,12 @@ class ScanPipeline:
         b.chunk_pt_off = d(cpo)
         self.hyp = HYP[hyp]
         if self.hyp == _lib.HYP_MT19937:
-            if mt_state is not None:
+            if isinstance(mt_state, DeviceArray):  # a device-resident chain, e.g. another call's mt_state_out
+                if mt_state.dtype != np.uint32 or mt_state.nbytes != S * 625 * 4:
+                    raise ValueError("device mt_state must be uint32 [n_scans, 625]")
+                self._keep.append(mt_state)
+                b.mt_state_in = mt_state.addr
+            elif mt_state is not None:
                 b.mt_state_in = d(np.ascontiguousarray(mt_state, np.uint32).reshape(S, 625))
             else:
                 b.seeds = d(np.ascontiguousarray(seeds if seeds is not None else np.arange(S), np.uint32))

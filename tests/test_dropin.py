@@ -29,10 +29,10 @@ def test_landmark_value_object():
     assert L.is_equal(M)  # ||pos_M - end_L|| = 0
     M.a = 0.7
     assert not L.is_equal(M)
-    lst = [L]
-    L.life = 0
-    landmarking.landmarks_track(lst)   # reference bug kept: never removes
-    assert lst == [L]
+    M.a = float("nan")
+    assert not L.is_equal(M)
+    sysm = systemClass.PoseHolder()
+    assert sysm.get_dim_x() == 3 and np.array_equal(sysm.get_pos(), np.zeros(3))
 
 
 def test_chunker_matches_functions_py():

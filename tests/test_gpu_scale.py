@@ -68,6 +68,47 @@ def test_c3_full_batch_properties(ctx):
         assert [L["id"] for L in lists[0]] == list(r1["landmarks"][s, :r1["lmk_count"][s]]["id"]), s
 
 
+def test_c2_full_batch_ransac_only(ctx):
+    """C2: 4096 x 720-pt scans through the RANSAC-only entry point (lslam_ransac, the
+    ransac_functions.py:23-31 leg: skimage ransac + a, b, tip per chunk).  Masks, every RANSAC
+    field of the chunk records and the MT streams equal the fused C3 run's; bit-exact against
+    the oracle on a sample of scans."""
+    import bench
+    from lidar_slam_amd.pipeline import ScanPipeline
+    from oracle import cpu as orc
+    ids = list(range(4096))
+    b, ukf = bench.make_workload(ids, 720, 20)
+    p = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
+                     want_state=True)
+    p.run_ransac_only()
+    r2 = p.results()
+    r3 = _run(ctx, b, ids, ukf)
+    m2, m3 = r2["models"], r3["models"]
+    assert np.array_equal(r2["mask"], r3["mask"])
+    assert np.array_equal(r2["mt_state"], r3["mt_state"])
+    for f in ("ox", "oy", "ux", "uy", "a", "b", "tip_x", "tip_y", "n_inliers", "best_trial", "n_draws",
+              "landmark_id", "n_points"):
+        assert np.array_equal(m2[f], m3[f]), f
+    assert np.array_equal(m2["flags"] & 63, m3["flags"] & 63)       # the RANSAC flags (no association bits)
+    assert np.all(m2["flags"] & 1) and not np.any(m2["flags"] & (64 | 128))
+    cpo, sco = b["chunk_pt_off"], b["scan_chunk_off"]
+    pop = np.add.reduceat(r2["mask"].astype(np.int64), cpo[:-1])
+    assert np.array_equal(pop, m2["n_inliers"])
+    # y_proj on the chunk's own line (no association pass)
+    sel = r2["mask"].astype(bool)
+    c_of_pt = np.repeat(np.arange(len(cpo) - 1), np.diff(cpo))
+    assert np.array_equal(r2["y_proj"][sel], m2["a"][c_of_pt[sel]] * b["xy"][sel, 0] + m2["b"][c_of_pt[sel]])
+    assert not np.any(r2["y_proj"][~sel])
+    for s in np.random.default_rng(2).choice(4096, 32, replace=False):
+        st = orc.MTState(seed=int(s))
+        for c in range(sco[s], sco[s + 1]):
+            mo, md, _ = orc.ransac(b["xy"][cpo[c]:cpo[c + 1]], 20.0, 100, state=st)
+            assert np.array_equal(r2["mask"][cpo[c]:cpo[c + 1]], mo), (s, c)
+            for f in ("best_trial", "n_draws", "flags", "n_inliers", "ox", "oy", "ux", "uy", "a", "b"):
+                assert m2[f][c] == md[f], (s, c, f)
+        assert np.array_equal(r2["mt_state"][s, :624], st.key) and r2["mt_state"][s, 624] == st.pos.value, s
+
+
 def test_c4_shard_8192(ctx):
     """Rank 1's shard of C4 (65,536 scans over 8 GPUs, `bench.py --gpus 8 --scans 8192`) equals
     the same scans run as two 4096-scan launches (ranks 2 and 3 of the default bench), and the
