@@ -3,13 +3,21 @@
 // Semantics: the INTENT of UKFMethods.py:10-71 + systemClass.py:7-29 (both files
 // fail to parse in the reference) run through filterpy 1.4.5's
 // UnscentedKalmanFilter (absent from the container; restated).  PARITY
-// UNPINNED — checked against the NumPy restatement in oracle/ukf.py.
+// UNPINNED — checked per component against a 50-digit evaluation of the same
+// algorithm (oracle/ukf_exact.py, tests/test_gpu_ukf_exact.py) and against the
+// NumPy restatement in oracle/ukf.py.
 //
 //   sigma points  MerweScaled: U = chol_upper((lambda+n) P); s0 = x,
 //                 s_{1+k} = x + U[k], s_{4+k} = x - U[k]
 //   fx            x + dt * B(theta) u,  B = [[R/2 c, R/2 c],[R/2 s, R/2 s],[-R/L, R/L]]
 //   hx            per landmark j: [sqrt(dx^2+dy^2), wrap(atan2(dy,dx) - theta)]
-//   means         linear weighted sums; angles by atan2(sum W sin, sum W cos)
+//   means         linear weighted sums; angles by atan2(sum W sin, sum W cos),
+//                 both evaluated about sigma point 0 (centred_mean): with
+//                 alpha = 1e-4 the float64 weights (~-1e8, 1.7e7) sum to
+//                 1 - 1.1e-8, so filterpy's literal sum sum(W s) is biased by
+//                 1.1e-8 |s| (3e-5 mm at 3 m), which reaches P as ~1e-5 relative
+//                 through the (Wc0 - Wm0) term.  s_0 + sum W (s - s_0) is the same
+//                 value in exact arithmetic and carries no such bias.
 //   residuals     differences with angle components wrapped to (-pi, pi]
 //   predict       x, P = UT(fx(sigmas)) + Q; sigmas_f re-drawn from (x, P)
 //   update        S = sum Wc rz rz^T + R, Pxz = sum Wc rx rz^T, K = Pxz S^-1,
@@ -154,20 +162,27 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             S.sig[3 * lane] = o[0];
             S.sig[3 * lane + 1] = o[1];
             S.sig[3 * lane + 2] = o[2];
-            S.tw[2 * lane] = ukf_sin(o[2]) * C.Wm[lane];
-            S.tw[2 * lane + 1] = ukf_cos(o[2]) * C.Wm[lane];
         }
         __syncthreads();
-        // UKFMethods.py:37-45 state_mean (intended form)
+        if (lane < 7) {
+            const double d = S.sig[3 * lane + 2] - S.sig[2];
+            S.tw[2 * lane] = ukf_sin(d) * C.Wm[lane];
+            S.tw[2 * lane + 1] = ukf_cos(d) * C.Wm[lane];
+        }
+        __syncthreads();
+        // UKFMethods.py:37-45 state_mean (intended form), evaluated about sigma point 0 (see
+        // centred_mean): sum Wm s = s_0 + sum Wm (s - s_0) and
+        // atan2(sum Wm sin a, sum Wm cos a) = a_0 + atan2(sum Wm sin(a - a_0), sum Wm cos(a - a_0))
         double s0 = 0.0, s1 = 0.0, ss = 0.0, sc = 0.0;
 #pragma unroll 1
         for (int k = 0; k < 7; k++) {
-            s0 += S.sig[3 * k] * C.Wm[k];
-            s1 += S.sig[3 * k + 1] * C.Wm[k];
+            s0 += (S.sig[3 * k] - S.sig[0]) * C.Wm[k];
+            s1 += (S.sig[3 * k + 1] - S.sig[1]) * C.Wm[k];
             ss += S.tw[2 * k];
             sc += S.tw[2 * k + 1];
         }
-        const double xm0 = s0, xm1 = s1, xm2 = ukf_atan2(ss, sc);
+        const double xm0 = S.sig[0] + s0, xm1 = S.sig[1] + s1;
+        const double xm2 = wrap_angle(S.sig[2] + ukf_atan2(ss, sc));
         // unscented_transform with residual_x (loop form) + Q
         double Pn[9];
         for (int i = 0; i < 9; i++) Pn[i] = 0.0;
@@ -220,11 +235,20 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         }
         S.Y[k * m2 + 2 * j] = d;
         S.Y[k * m2 + 2 * j + 1] = ph;
-        S.wsc[k * m2 + 2 * j] = ukf_sin(ph) * C.Wm[k];
-        S.wsc[k * m2 + 2 * j + 1] = ukf_cos(ph) * C.Wm[k];
     }
     __syncthreads();
-    // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals
+    // Wm-weighted sin / cos of each bearing about sigma 0's (the centred z_mean, below)
+#pragma unroll 1
+    for (int e = lane; e < npair; e += 64) {
+        const int k = e / C.L, j = e - k * C.L;
+        const double dph = S.Y[k * m2 + 2 * j + 1] - S.Y[2 * j + 1];
+        S.wsc[k * m2 + 2 * j] = ukf_sin(dph) * C.Wm[k];
+        S.wsc[k * m2 + 2 * j + 1] = ukf_cos(dph) * C.Wm[k];
+    }
+    __syncthreads();
+    // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals.
+    // UKFMethods.py:47-57 about sigma 0 (as state_mean above): dm = d_0 + sum Wm (d - d_0),
+    // pm = phi_0 + atan2(sum Wm sin(phi - phi_0), sum Wm cos(phi - phi_0)).
 #pragma unroll 1
     for (int j = lane; j < C.L; j += 64) {
         double px, py;
@@ -235,11 +259,12 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         }
         double dm = 0.0, ss = 0.0, sc = 0.0;
         for (int k = 0; k < 7; k++) {
-            dm += S.Y[k * m2 + 2 * j] * C.Wm[k];
+            dm += (S.Y[k * m2 + 2 * j] - S.Y[2 * j]) * C.Wm[k];
             ss += S.wsc[k * m2 + 2 * j];
             sc += S.wsc[k * m2 + 2 * j + 1];
         }
-        const double pm = ukf_atan2(ss, sc);
+        dm = S.Y[2 * j] + dm;
+        const double pm = wrap_angle(S.Y[2 * j + 1] + ukf_atan2(ss, sc));
         S.wsc[2 * j] = dm;  // row 0 of wsc is consumed: (dm, pm) per landmark
         S.wsc[2 * j + 1] = pm;
         S.yr[2 * j] = z[2 * j] - dm;

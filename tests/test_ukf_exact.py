@@ -1,0 +1,58 @@
+"""The UKF's float64 rounding against a 50-digit evaluation of the same algorithm
+(oracle/ukf_exact.py, fixtures tests/golden/ukf_exact.npz).
+
+PARITY UNPINNED for the algorithm (the reference UKF does not parse, filterpy is
+absent); these tests bound the implementations' ROUNDING per component against
+north_star's 1e-5: x and y relative, theta absolute (rad), P relative to max|P|.
+The CPU side checks the exact evaluator (dense S^-1 = Woodbury, the fixtures
+regenerate) and the NumPy oracle's own error; tests/test_gpu_ukf_exact.py holds
+the HIP kernel to the same bounds."""
+import numpy as np
+import pytest
+
+from oracle import ukf as oukf
+from oracle import ukf_exact as ux
+
+TOL = {"x_rel": 1e-5, "y_rel": 1e-5, "theta_abs": 1e-5, "P_rel": 1e-5}
+CASES = ("c3", "c5", "bench", "map", "predict")
+
+
+def case(golden, name):
+    g = golden("ukf_exact.npz")
+    return {k[len(name) + 1:]: v for k, v in g.items() if k.startswith(name + "_")}
+
+
+def test_woodbury_equals_dense_inverse(golden):
+    c = case(golden, "c3")
+    for s in (0, 1):
+        args = (c["x"][s], c["P"][s], c["u"][s], c["z"][s], c["lmk"][s], c["R_diag"])
+        xw, Pw = ux.to_float(*ux.step(*args))
+        xd, Pd = ux.to_float(*ux.step(*args, dense=True))
+        assert np.array_equal(xw, xd) and np.array_equal(Pw, Pd)
+
+
+def test_fixtures_regenerate(golden):
+    for name, idx in (("c3", (0, 4)), ("c5", (0,)), ("map", (1,)), ("predict", (2,))):
+        c = case(golden, name)
+        for s in idx:
+            x, P = ux.to_float(*ux.step(c["x"][s], c["P"][s], c["u"][s], c["z"][s], c["lmk"][s], c["R_diag"],
+                                        update=bool(c["flags"] & 2)))
+            assert np.array_equal(x, c["x_exact"][s]) and np.array_equal(P, c["P_exact"][s]), (name, s)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_float64_oracle_rounding_per_component(golden, name):
+    c = case(golden, name)
+    upd = bool(c["flags"] & 2)
+    xo, Po = oukf.ukf_batch(c["x"], c["P"], c["u"], c["z"], c["lmk"], c["R_diag"], update=upd)
+    err = ux.component_errors(xo, Po, c["x_exact"], c["P_exact"])
+    for k, tol in TOL.items():
+        assert err[k] <= tol, (name, err)
+
+
+def test_exact_step_is_not_the_float64_one(golden):
+    """The fixtures carry information: the float64 oracle differs from them (else the bound
+    above would be vacuous)."""
+    c = case(golden, "c3")
+    xo, Po = oukf.ukf_batch(c["x"], c["P"], c["u"], c["z"], c["lmk"], c["R_diag"])
+    assert not np.array_equal(xo, c["x_exact"]) and not np.array_equal(Po, c["P_exact"])
