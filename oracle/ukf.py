@@ -81,6 +81,33 @@ def z_mean(sigmas, Wm):
     return x
 
 
+# The same means evaluated about sigma point 0: sum W s = s_0 + sum W (s - s_0) and
+# atan2(sum W sin a, sum W cos a) = a_0 + atan2(sum W sin(a - a_0), sum W cos(a - a_0)),
+# identical in exact arithmetic (the weights sum to 1).  In float64 the alpha = 1e-4
+# weights (~-1e8, 1.7e7) sum to 1 - 1.1e-8, which biases the literal sums by 1.1e-8 |s|
+# and, through the (Wc0 - Wm0) term of the covariance, P by ~1e-5 relative
+# (tests/test_ukf_exact.py measures both forms against a 50-digit evaluation).  The HIP
+# kernel (lslam_ukf.h) uses this form.
+def state_mean_centred(sigmas, Wm):
+    d = sigmas - sigmas[0]
+    x = np.zeros(3)
+    x[0] = sigmas[0, 0] + np.dot(d[:, 0], Wm)
+    x[1] = sigmas[0, 1] + np.dot(d[:, 1], Wm)
+    x[2] = normalize_angle(sigmas[0, 2] + math.atan2(np.dot(np.sin(d[:, 2]), Wm), np.dot(np.cos(d[:, 2]), Wm)))
+    return x
+
+
+def z_mean_centred(sigmas, Wm):
+    n = sigmas.shape[1]
+    d = sigmas - sigmas[0]
+    x = np.zeros(n)
+    for z in range(0, n, 2):
+        x[z] = sigmas[0, z] + np.dot(d[:, z], Wm)
+        x[z + 1] = normalize_angle(sigmas[0, z + 1] + math.atan2(np.dot(np.sin(d[:, z + 1]), Wm),
+                                                                 np.dot(np.cos(d[:, z + 1]), Wm)))
+    return x
+
+
 def residual_x(a, b):
     y = a - b
     y[2] = normalize_angle(y[2])
@@ -132,7 +159,7 @@ class UKF:
     """filterpy UnscentedKalmanFilter as configured by systemClass.py:21-29."""
 
     def __init__(self, n_landmarks, dt=DT, alpha=1e-4, beta=2.0, kappa=0.0, fx=transition_function,
-                 hx=transfer_function, x_mean=state_mean, z_mean_fn=z_mean, res_x=residual_x,
+                 hx=transfer_function, x_mean=state_mean_centred, z_mean_fn=z_mean_centred, res_x=residual_x,
                  res_z=residual_h):
         self.points = MerweScaledSigmaPoints(3, alpha, beta, kappa)
         self.Wm, self.Wc = self.points.Wm, self.points.Wc
@@ -169,14 +196,16 @@ class UKF:
         self.P = self.P - np.dot(K, np.dot(S, K.T))
 
 
-def ukf_batch(x, P, u, z, lmk, R_diag, dt=DT, predict=True, update=True, Q=None):
-    """Run one predict/update per scan; returns (x[S,3], P[S,3,3])."""
+def ukf_batch(x, P, u, z, lmk, R_diag, dt=DT, predict=True, update=True, Q=None, centred=True):
+    """Run one predict/update per scan; returns (x[S,3], P[S,3,3]).  ``centred=False``: filterpy's
+    literal float64 means (state_mean / z_mean above) instead of the centred form."""
     S = x.shape[0]
     L = lmk.shape[1]
     xo = np.zeros((S, 3))
     Po = np.zeros((S, 3, 3))
+    means = {} if centred else dict(x_mean=state_mean, z_mean_fn=z_mean)
     for s in range(S):
-        f = UKF(L, dt=dt)
+        f = UKF(L, dt=dt, **means)
         f.x = np.array(x[s], np.float64)
         f.P = np.array(P[s], np.float64).reshape(3, 3)
         f.R = np.diag(np.asarray(R_diag, np.float64))

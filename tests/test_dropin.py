@@ -104,8 +104,9 @@ def test_system_ukf_vs_oracle():
     f.x = np.array([1000.0, 800.0, 0.3])
     f.predict(np.array([2.0, 2.5]))
     f.update(z, lm)
-    assert np.max(np.abs(sysm.ukf.x - f.x)) < 1e-4
-    assert np.max(np.abs(sysm.ukf.P - f.P)) < 1e-6
+    from oracle import ukf_exact
+    err = ukf_exact.component_errors(sysm.ukf.x[None], sysm.ukf.P[None], f.x[None], f.P[None])
+    assert max(err.values()) <= 1e-5, err
 
 
 @pytest.mark.gpu

@@ -53,33 +53,15 @@ def test_linear_ukf_equals_kalman():
     assert np.allclose(f.x, x, atol=1e-10) and np.allclose(f.P, P, atol=1e-10)
 
 
-def _exact_state_mean(sigmas, Wm):
-    x = np.zeros(3)
-    x[0] = math.fsum(sigmas[:, 0] * Wm)
-    x[1] = math.fsum(sigmas[:, 1] * Wm)
-    x[2] = math.atan2(math.fsum(np.sin(sigmas[:, 2]) * Wm), math.fsum(np.cos(sigmas[:, 2]) * Wm))
-    return x
-
-
-def test_noise_floor_of_alpha_1e4():
-    """Two summation orders of the SAME algorithm differ at the level the GPU
-    parity tolerance allows (|dx| ~1e-6..1e-4, |dP| ~1e-8): the floor is the
-    cancellation of the +-1e8 weights, not an implementation error."""
+def test_centred_means_equal_literal_up_to_the_weight_sum():
+    """state_mean_centred and state_mean are the same mean; in float64 they differ by the
+    literal form's bias (1 - sum Wm) * s (sum Wm = 1 - 1.1e-8 for alpha = 1e-4)."""
     rng = np.random.default_rng(11)
-    dxs, dPs = [], []
-    for s in range(16):
-        L = 20
-        x0 = np.array([rng.uniform(800, 3200), rng.uniform(800, 2200), rng.uniform(-np.pi, np.pi)])
-        lmk = [tuple(p) for p in rng.uniform(-3000, 3000, (L, 2))]
-        z = oukf.transfer_function(x0, lmk) + rng.normal(0, 0.3, 2 * L)
-        outs = []
-        for mean_fn in (oukf.state_mean, _exact_state_mean):
-            f = oukf.UKF(L, x_mean=mean_fn)
-            f.x = x0.copy()
-            f.predict(np.array([2.0, 2.5]))
-            f.update(z, lmk)
-            outs.append((f.x.copy(), f.P.copy()))
-        dxs.append(np.max(np.abs(outs[0][0] - outs[1][0])))
-        dPs.append(np.max(np.abs(outs[0][1] - outs[1][1])))
-    assert max(dPs) < 1e-6 and max(dxs) < 1e-4
-    assert max(dPs) > 1e-10  # the spread is real, not zero
+    pts = oukf.MerweScaledSigmaPoints(3, 1e-4, 2.0, 0.0)
+    bias = 1.0 - math.fsum(pts.Wm)
+    for _ in range(16):
+        x0 = np.array([rng.uniform(800, 3200), rng.uniform(800, 2200), rng.uniform(-3.0, 3.0)])
+        sig = pts.sigma_points(x0, np.diag([.1, .1, .05]))
+        lit, cen = oukf.state_mean(sig, pts.Wm), oukf.state_mean_centred(sig, pts.Wm)
+        assert np.all(np.abs(lit[:2] - cen[:2]) <= 3 * abs(bias) * np.abs(x0[:2]) + 1e-9)
+        assert abs(lit[2] - cen[2]) < 1e-7
