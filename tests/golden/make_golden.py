@@ -15,6 +15,7 @@ box except the ``.npz`` files.
 
 Files written next to this script:
   mt_choice.npz   legacy MT19937 seeding / raw words / choice(N,2,replace=False)
+  batch256.npz    256 scans, lean: per-chunk results + pre-call lists (points regenerated)
   batch.npz       24 independent scans, np.random.seed(s) per scan, fresh
                   landmark list per scan (the batched API's semantics)
   live.npz        one chained run: ONE np.random.seed, ONE landmark list over
@@ -222,6 +223,75 @@ def gen_batch(n_scans=24):
                seeds=np.asarray(ids, np.uint32))
     np.savez_compressed(os.path.join(HERE, "batch.npz"), **out)
     print("batch.npz", out["xy"].shape, len(out["a"]), "chunks")
+
+
+def gen_batch256(n_scans=256):
+    """SURVEY §8(c)'s ~256-scan plan, kept lean (~1 MB): the points are NOT stored (synth's
+    generator regenerates them bit for bit under numpy 1.26 and 2.x; their sha256 is), nor
+    the draws or MT states (batch.npz / mt_choice.npz pin those; here a hash of each scan's
+    final state).  Per chunk: mask, per-trial counts, winner, draws used, origin, direction,
+    a, b, tip, new-landmark flag, and the pre-call landmark list with every field (the
+    association decisions, is_equal at landmarking.py:66-77, are replayed from it)."""
+    import hashlib
+    ids = list(range(n_scans))
+    b = synth.make_batch(ids)
+    r = {k: [] for k in ("mask", "trial_cnt", "best_trial", "draws_used", "n_inl", "origin", "direction", "a", "b",
+                         "tip", "new_landmark")}
+    lin = {k: [] for k in ("id", "life", "a", "b", "pos", "end")}
+    lin_off, lout_id, lout_life, lout_off = [0], [], [], [0]
+    state_hash = []
+    for s in ids:
+        np.random.seed(s)
+        landmarks = []
+        for c in range(b["scan_chunk_off"][s], b["scan_chunk_off"][s + 1]):
+            data = b["xy"][b["chunk_pt_off"][c]:b["chunk_pt_off"][c + 1]]
+            st0 = np.random.get_state()
+            draws, _ = replay_draws(st0, data.shape[0], T + 1)
+            cnt, sm = trial_stats(data, draws, T, THR)
+            bt, stop = best_trial(cnt, sm)
+            np.random.set_state(st0)
+            model, inl = ransac(data, LineModelND, min_samples=rf.MIN_SAMPLES, residual_threshold=THR, max_trials=T)
+            Recorder._dump_list(lin, lin_off, landmarks)
+            np.random.set_state(st0)
+            q, fitted, new = _silent(rf.landmark_extraction, [data.tolist()], c - b["scan_chunk_off"][s], landmarks)
+            if new:
+                landmarks.append(fitted)
+            r["mask"].append(inl.astype(np.uint8))
+            r["trial_cnt"].append(cnt.astype(np.uint8))
+            r["best_trial"].append(bt)
+            r["draws_used"].append(stop + 2)
+            r["n_inl"].append(int(inl.sum()))
+            r["origin"].append(np.asarray(model.params[0], np.float64))
+            r["direction"].append(np.asarray(model.params[1], np.float64))
+            r["a"].append(fitted.a)
+            r["b"].append(fitted.b)
+            r["tip"].append(np.asarray(fitted.end, np.float64))
+            r["new_landmark"].append(bool(new))
+            lout_id.extend(L.id for L in landmarks)
+            lout_life.extend(L.life for L in landmarks)
+            lout_off.append(len(lout_id))
+        st = np.random.get_state()
+        state_hash.append(int.from_bytes(hashlib.sha256(st[1].tobytes() + np.int32(st[2]).tobytes()).digest()[:8],
+                                         "little"))
+    out = dict(
+        n_scans=np.int32(n_scans),
+        xy_sha256=np.frombuffer(hashlib.sha256(b["xy"].tobytes()).digest(), np.uint8),
+        scan_chunk_off=b["scan_chunk_off"], chunk_pt_off=b["chunk_pt_off"], seeds=np.asarray(ids, np.uint32),
+        mask=np.concatenate(r["mask"]), trial_cnt=np.asarray(r["trial_cnt"], np.uint8),
+        best_trial=np.asarray(r["best_trial"], np.int32), draws_used=np.asarray(r["draws_used"], np.int32),
+        n_inl=np.asarray(r["n_inl"], np.int32), origin=np.asarray(r["origin"]), direction=np.asarray(r["direction"]),
+        a=np.asarray(r["a"]), b=np.asarray(r["b"]), tip=np.asarray(r["tip"]),
+        new_landmark=np.asarray(r["new_landmark"], np.uint8),
+        lm_in_off=np.asarray(lin_off, np.int32), lm_in_id=np.asarray(lin["id"], np.int32),
+        lm_in_life=np.asarray(lin["life"], np.int32), lm_in_a=np.asarray(lin["a"], np.float64),
+        lm_in_b=np.asarray(lin["b"], np.float64), lm_in_pos=np.asarray(lin["pos"], np.float64).reshape(-1, 2),
+        lm_in_end=np.asarray(lin["end"], np.float64).reshape(-1, 2),
+        lm_out_off=np.asarray(lout_off, np.int32), lm_out_id=np.asarray(lout_id, np.int32),
+        lm_out_life=np.asarray(lout_life, np.int32),
+        state_after_hash=np.asarray(state_hash, np.uint64))
+    np.savez_compressed(os.path.join(HERE, "batch256.npz"), **out)
+    print("batch256.npz", len(out["a"]), "chunks,", os.path.getsize(os.path.join(HERE, "batch256.npz")), "bytes;",
+          "matches:", int((out["new_landmark"] == 0).sum()))
 
 
 def gen_live(n_scans=14, seed=20240611):
@@ -493,7 +563,7 @@ def gen_known():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["mt", "batch", "live", "edge", "assoc", "big", "known"]
+    which = sys.argv[1:] or ["mt", "batch", "batch256", "live", "edge", "assoc", "big", "known"]
     t0 = time.time()
     if "mt" in which:
         gen_mt_choice()
@@ -505,6 +575,8 @@ if __name__ == "__main__":
         gen_assoc()
     if "batch" in which:
         gen_batch()
+    if "batch256" in which:
+        gen_batch256()
     if "live" in which:
         gen_live()
     if "big" in which:

@@ -462,3 +462,40 @@ def test_border_band_and_degenerate_hypotheses(ctx, large):
                 assert m[f][c] == md[f] or (np.isnan(m[f][c]) and np.isnan(md[f])), (s, c, f)
             c += 1
         assert np.array_equal(r["mt_state"][s, :624], st.key) and r["mt_state"][s, 624] == st.pos.value, s
+
+
+def test_batch256_pipeline_vs_reference(ctx, golden):
+    """The 256-scan reference batch (tests/golden/batch256.npz) through the fused pipeline:
+    masks, per-trial counts, winners, draws used, origins exact; directions <= 1e-11; a, b,
+    tip_y <= 1e-9 relative; new-landmark decisions, each scan's final list (ids, lives) and
+    final MT state (hash) exact."""
+    import hashlib
+
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import ScanPipeline
+    g = golden("batch256.npz")
+    S = int(g["n_scans"])
+    b = synth.make_batch(list(range(S)))
+    assert hashlib.sha256(b["xy"].tobytes()).digest() == g["xy_sha256"].tobytes()
+    p = ScanPipeline(ctx, b["xy"], g["scan_chunk_off"], g["chunk_pt_off"], seeds=g["seeds"], lmk_capacity=64,
+                     want_counts=True, want_state=True)
+    p.run()
+    r = p.results()
+    m = r["models"]
+    assert np.array_equal(r["mask"], g["mask"])
+    assert np.array_equal(r["counts"].astype(np.uint8), g["trial_cnt"])
+    assert np.array_equal(m["best_trial"], g["best_trial"]) and np.array_equal(m["n_draws"], g["draws_used"])
+    assert np.array_equal(m["n_inliers"], g["n_inl"])
+    assert np.array_equal(m["ox"], g["origin"][:, 0]) and np.array_equal(m["oy"], g["origin"][:, 1])
+    assert _dir_ok(m["ux"], m["uy"], g["direction"])
+    assert np.all(_rel(m["a"], g["a"]) < REL) and np.all(_rel(m["b"], g["b"]) < REL)
+    assert np.array_equal(m["tip_x"], g["tip"][:, 0]) and np.all(_rel(m["tip_y"], g["tip"][:, 1]) < REL)
+    assert np.array_equal((m["flags"] & 64) != 0, g["new_landmark"].astype(bool))
+    for s in range(S):
+        c = g["scan_chunk_off"][s + 1] - 1
+        l0, l1 = g["lm_out_off"][c], g["lm_out_off"][c + 1]
+        lst = r["landmarks"][s, :r["lmk_count"][s]]
+        assert list(lst["id"]) == list(g["lm_out_id"][l0:l1]) and list(lst["life"]) == list(g["lm_out_life"][l0:l1])
+        st = r["mt_state"][s]
+        h = int.from_bytes(hashlib.sha256(st[:624].tobytes() + np.int32(st[624]).tobytes()).digest()[:8], "little")
+        assert h == int(g["state_after_hash"][s]), s
