@@ -5,7 +5,7 @@ python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
          --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (config C3 of BASELINE.json, per GPU): 4096 synthetic 720-point scans
+Main line (config C3 of BASELINE.json, per GPU): 4096 synthetic 720-point scans
 (SURVEY §8d generator), chunked 7x100 + 20 as functions.py:64-76 does; per
 chunk skimage-semantics RANSAC (100 trials, 20 mm, numpy legacy MT19937 stream
 seeded per scan: results identical to the reference), landmark association
@@ -15,6 +15,11 @@ of lslam_scan_pipeline.  Inputs are resident in HBM before timing.  Multi-GPU:
 each rank owns its own 4096 scans (ids rank*4096 ...), no data-path
 collective; torch.distributed (gloo) is used only for the barrier and the
 max-over-ranks of the elapsed time.
+
+C4 leg (configs[3]; at N > 1 by default, or --c4): one host batch of 65,536
+scans in shared memory split across the ranks, H2D + pipeline + RCCL gather of
+the results to rank 0 + D2H, timed end to end (the "c4" object of the line;
+c4_leg below).
 """
 from __future__ import annotations
 
@@ -178,6 +183,150 @@ def load_traffic(path):
         return None
 
 
+C4_FIELDS = ("mask", "models", "ukf_x", "ukf_P", "lmk_count")
+
+
+def c4_leg(args, rank, world, dist, ctx, L):
+    """BASELINE configs[3] (C4): ONE host batch of ``--c4-scans`` scans split across the ranks,
+    end to end.  The batch lives in one shared-memory segment of the node (the stand-in for
+    the reference's mp.Queue hand-off, SLAM.py:13,18-23): rank 0 creates it, each rank fills
+    its own shard (the generator is per scan) and page-locks the segment.  Per timed step,
+    every rank H2Ds its shard's inputs, runs the fused pipeline on them, and the per-scan
+    results (inlier masks, chunk records, UKF x / P, landmark counts) are gathered to rank 0's
+    HBM over RCCL (lidar_slam_amd.collective: grouped send / recv on the context stream), then
+    copied to rank 0's host.  Timed like the main line: barrier + sync on both sides, max over
+    ranks.  Returns the JSON object of the leg."""
+    from multiprocessing import shared_memory
+
+    from lidar_slam_amd import shard, synth
+    total = int(args.c4_scans)
+    sizes = synth.chunk_sizes(args.beams)
+    nch, npt = len(sizes), int(sum(sizes))
+    sco = (np.arange(total + 1) * nch).astype(np.int32)
+    cpo = np.concatenate([[0], np.cumsum(np.tile(sizes, total))]).astype(np.int32)
+    plan = shard.plan(sco, cpo, world)
+    # the shared host batch: xy | seeds | x | P | u | z | lmk | R_diag, page-aligned parts
+    layout, off = {}, 0
+    for name, shape, dt in (("xy", (total * npt, 2), np.float64), ("seeds", (total,), np.uint32),
+                            ("ukf_x", (total, 3), np.float64), ("ukf_P", (total, 3, 3), np.float64),
+                            ("ukf_u", (total, 2), np.float64), ("ukf_z", (total, 2 * L), np.float64),
+                            ("ukf_lmk", (total, L, 2), np.float64), ("ukf_R_diag", (2 * L,), np.float64)):
+        nb = int(np.prod(shape)) * np.dtype(dt).itemsize
+        layout[name] = (off, shape, dt)
+        off = (off + nb + 4095) & ~4095
+    seg_name = ["lslam_c4_%d_%d" % (os.getpid(), int(time.time()))]
+    shm = None
+    try:
+        if rank == 0:
+            shm = shared_memory.SharedMemory(name=seg_name[0], create=True, size=off)
+        if dist is not None:
+            dist.broadcast_object_list(seg_name, 0)
+            if rank != 0:
+                shm = shared_memory.SharedMemory(name=seg_name[0])
+        return _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan)
+    finally:
+        if dist is not None:
+            dist.barrier()
+        if shm is not None:
+            try:
+                shm.close()
+            except BufferError:  # views still referenced (an exception's traceback): the OS reclaims it
+                pass
+            if rank == 0:
+                shm.unlink()
+
+
+def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
+    from lidar_slam_amd import collective, shard
+    from lidar_slam_amd.device import DeviceArray, register_host, unregister_host
+    from lidar_slam_amd.pipeline import ScanPipeline
+    me = plan[rank]
+    total = len(sco) - 1
+    seg = np.ndarray((off,), np.uint8, buffer=shm.buf)
+    host = {k: np.ndarray(shape, dt, buffer=shm.buf, offset=o) for k, (o, shape, dt) in layout.items()}
+    ids = list(range(me.lo, me.hi))
+    b, wk = make_workload(ids, args.beams, L, seed_base=1000 + rank)
+    host["xy"][me.p0:me.p1] = b["xy"]
+    host["seeds"][me.lo:me.hi] = ids
+    for k in ("x", "P", "u", "z", "lmk"):
+        host["ukf_" + k][me.lo:me.hi] = wk[k].reshape(host["ukf_" + k][me.lo:me.hi].shape)
+    if rank == 0:
+        host["ukf_R_diag"][:] = wk["R_diag"]
+    del b, wk
+    if dist is not None:
+        dist.barrier()
+    pinned = register_host(seg)
+    mine = me.inputs(dict(host, scan_chunk_off=sco, chunk_pt_off=cpo))
+    ukf = dict(n_landmarks=L, **{k: mine["ukf_" + k] for k in ("x", "P", "u", "z", "lmk", "R_diag")})
+    pipe = ScanPipeline(ctx, mine["xy"], mine["scan_chunk_off"], mine["chunk_pt_off"], seeds=mine["seeds"],
+                        max_trials=args.trials, lmk_capacity=args.lmk_capacity, want_yproj=False, ukf=ukf)
+    comm = collective.Comm.from_process_group(ctx, dist)
+    local = {"mask": pipe.mask, "models": pipe.models, "ukf_x": pipe.ukf_x, "ukf_P": pipe.ukf_P,
+             "lmk_count": pipe.lmk_count}
+    recv, host_out = {}, {}
+    if rank == 0:
+        for k in C4_FIELDS:
+            nb = sum(s.field_bytes(args.lmk_capacity)[k] for s in plan)
+            recv[k] = DeviceArray(ctx, (nb,), np.uint8)
+            host_out[k] = np.empty(nb, np.uint8)
+            register_host(host_out[k])
+    upload = {k: mine[k] for k in ("xy", "seeds", "ukf_u", "ukf_z", "ukf_lmk", "ukf_x", "ukf_P")}
+
+    def h2d():
+        pipe.upload_async(**upload)
+        pipe.clear_lists_async()
+
+    def compute():
+        pipe.run(sync=False)
+
+    def gather():
+        shard.gather(plan, rank, local, comm.gatherv, lambda k, n: recv[k], lmk_capacity=args.lmk_capacity)
+
+    def d2h():
+        for k in (C4_FIELDS if rank == 0 else ()):
+            recv[k].download_async(host_out[k])
+
+    def step():
+        h2d()
+        compute()
+        gather()
+        d2h()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    elapsed = reduce_max(timed_region(step, args.c4_steps, args.warmup, ctx.sync, barrier), dist)
+    phases = {}
+    for name, fn in (("h2d", h2d), ("pipeline", compute), ("gather", gather), ("d2h", d2h)):
+        ts = [timed_region(fn, 1, 0, ctx.sync, barrier) for _ in range(3)]
+        phases[name + "_ms"] = round(reduce_max(float(np.median(ts)), dist) * 1e3, 4)
+    res = {"workload": "C4: %d synthetic %d-pt scans in one shared host batch, %d shards of %d-%d scans; per step "
+                       "H2D + fused RANSAC/association/UKF pipeline + RCCL gather of masks, chunk records, UKF x/P "
+                       "and landmark counts to rank 0 + D2H there"
+                       % (total, args.beams, world, min(s.n_scans for s in plan), max(s.n_scans for s in plan)),
+           "total_scans": total, "steps": args.c4_steps, "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
+           "e2e_scans_per_s": round(total * args.c4_steps / elapsed, 1), "phases_alone": phases,
+           "gathered_bytes_per_step": int(sum(v.nbytes for v in host_out.values())) if rank == 0 else None,
+           "host_batch": "shared memory, %s" % ("page-locked" if pinned else "pageable"),
+           "rccl_version": collective.version(), "transport": "RCCL grouped send/recv on the lslam context stream"}
+    if rank == 0:
+        m = shard.host_view("models", host_out["models"], total)
+        pop = np.add.reduceat(host_out["mask"].astype(np.int64), cpo[:-1])
+        x = shard.host_view("ukf_x", host_out["ukf_x"], total)
+        res["consistent"] = bool(np.all(m["flags"] & 1) and np.array_equal(pop, m["n_inliers"]) and
+                                 np.all(np.isfinite(x)) and np.array_equal(m["n_points"], np.diff(cpo)))
+        res["capacity_overflows"] = capacity_overflows(m)
+        for v in host_out.values():
+            unregister_host(v)
+    comm.close()
+    del pipe, local, recv
+    ctx.sync()
+    if pinned:
+        unregister_host(seg)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,6 +346,10 @@ def main():
                     help="per-scan landmark list capacity (>= the steady-state list, ~42 on C3)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     ap.add_argument("--also-philox", action="store_true", help="also time the Philox (throughput) mode")
+    ap.add_argument("--c4", action="store_true", help="run the C4 leg (also at one GPU; default: only N > 1)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg at N > 1")
+    ap.add_argument("--c4-scans", type=int, default=65536, help="C4: scans of the one shared batch")
+    ap.add_argument("--c4-steps", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,8 +373,10 @@ def main():
 
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
 
     from lidar_slam_amd import _lib
     from lidar_slam_amd.device import Context
@@ -356,6 +511,11 @@ def main():
             pipe2.run(sync=False)
         ctx.sync()
         out["philox_scans_per_s"] = round(S * args.steps / (time.perf_counter() - t0), 1)
+    if args.c4 or (world > 1 and not args.no_c4):
+        try:
+            out["c4"] = c4_leg(args, rank, world, dist, ctx, L)
+        except Exception as e:  # the main line stands on its own; report the leg's failure in it
+            out["c4"] = {"error": "%s: %s" % (type(e).__name__, e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

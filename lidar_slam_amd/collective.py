@@ -1,0 +1,169 @@
+"""RCCL over xGMI for the sharded path's one data movement: every rank's per-scan
+results to the root, plus the bootstrap and a broadcast.
+
+ctypes on ROCm's librccl (rccl.h: ncclGetUniqueId :187, ncclCommInitRank :220,
+ncclBroadcast :591, ncclSend :700, ncclRecv :722, ncclGroupStart/End :923-933).
+One process per GPU; the 128-byte unique id travels over the host process group
+(gloo).  Every collective is enqueued on the lslam context's main stream
+(lslam_ctx_stream), so it runs after the pipeline call that wrote its buffers and
+before the context's later calls, with no host sync.
+
+``gatherv`` is the variable-size gather as grouped point-to-point operations: the
+root receives rank r's bytes at offset sum(counts[:r]) from each peer (one xGMI
+link per peer, all in flight together) and copies its own with a device copy;
+every other rank sends once.  Shards of 65,536 720-point scans over 8 ranks are
+equal, but the CSR layout allows ragged shards, which plain ncclGather does not.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from .device import DeviceArray
+
+NCCL_UINT8 = 1  # rccl.h ncclDataType_t
+
+
+class RcclError(RuntimeError):
+    pass
+
+
+class UniqueId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
+_rccl = None
+
+
+def load():
+    global _rccl
+    if _rccl is not None:
+        return _rccl
+    err = None
+    for name in ("librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so"):
+        try:
+            L = C.CDLL(name)
+            break
+        except OSError as e:
+            err = e
+    else:
+        raise RcclError("cannot load librccl: %s" % err)
+    VP, I, SZ = C.c_void_p, C.c_int, C.c_size_t
+    L.ncclGetUniqueId.argtypes = [C.POINTER(UniqueId)]
+    L.ncclCommInitRank.argtypes = [C.POINTER(VP), I, UniqueId, I]
+    L.ncclCommDestroy.argtypes = [VP]
+    L.ncclGetErrorString.argtypes = [I]
+    L.ncclGetErrorString.restype = C.c_char_p
+    L.ncclSend.argtypes = [VP, SZ, I, I, VP, VP]
+    L.ncclRecv.argtypes = [VP, SZ, I, I, VP, VP]
+    L.ncclBroadcast.argtypes = [VP, VP, SZ, I, I, VP, VP]
+    L.ncclGetVersion.argtypes = [C.POINTER(I)]
+    for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclSend", "ncclRecv", "ncclBroadcast",
+              "ncclGroupStart", "ncclGroupEnd", "ncclGetVersion"):
+        getattr(L, f).restype = I
+    _rccl = L
+    return L
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RcclError("%s: %s" % (what, load().ncclGetErrorString(rc).decode(errors="replace")))
+
+
+def version():
+    v = C.c_int(0)
+    _check(load().ncclGetVersion(C.byref(v)), "ncclGetVersion")
+    return v.value
+
+
+def unique_id() -> bytes:
+    uid = UniqueId()
+    _check(load().ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+    return bytes(bytearray(uid.internal))
+
+
+def _addr(x, off=0):
+    base = x.addr if isinstance(x, DeviceArray) else int(x)
+    return C.c_void_p(base + int(off))
+
+
+class Comm:
+    """One rank of an RCCL communicator bound to an lslam context (its device and stream)."""
+
+    def __init__(self, ctx, world: int, rank: int, uid: bytes):
+        L = load()
+        self.ctx, self.world, self.rank = ctx, int(world), int(rank)
+        u = UniqueId()
+        C.memmove(C.addressof(u), uid, 128)
+        self._comm = C.c_void_p()
+        ctx.sync()  # ncclCommInitRank binds the calling thread's current device: the context's
+        _check(L.ncclCommInitRank(C.byref(self._comm), self.world, u, self.rank), "ncclCommInitRank")
+
+    @classmethod
+    def from_process_group(cls, ctx, dist=None):
+        """Bootstrap over torch.distributed (gloo): rank 0's unique id broadcast to all."""
+        world = dist.get_world_size() if dist is not None else 1
+        rank = dist.get_rank() if dist is not None else 0
+        if world == 1:
+            return cls(ctx, 1, 0, unique_id())
+        import torch
+        buf = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+        dist.broadcast(buf, 0)
+        return cls(ctx, world, rank, bytes(buf.numpy().tobytes()))
+
+    @property
+    def _stream(self):
+        return C.c_void_p(self.ctx.stream)
+
+    def gatherv(self, send, recv, counts, root=0):
+        """Rank r's first counts[r] bytes of ``send`` -> ``recv`` at sum(counts[:r]) on root."""
+        L = load()
+        offs = [0]
+        for n in counts:
+            offs.append(offs[-1] + int(n))
+        st = self._stream
+        if self.rank == root and counts[root]:
+            self.ctx.copy(_addr(recv, offs[root]).value, _addr(send).value, counts[root])
+        if self.world == 1:
+            return
+        _check(L.ncclGroupStart(), "ncclGroupStart")
+        try:
+            if self.rank == root:
+                for r in range(self.world):
+                    if r != root and counts[r]:
+                        _check(L.ncclRecv(_addr(recv, offs[r]), int(counts[r]), NCCL_UINT8, r, self._comm, st),
+                               "ncclRecv")
+            elif counts[self.rank]:
+                _check(L.ncclSend(_addr(send), int(counts[self.rank]), NCCL_UINT8, root, self._comm, st), "ncclSend")
+        finally:
+            _check(L.ncclGroupEnd(), "ncclGroupEnd")
+
+    def broadcast(self, buf, nbytes, root=0):
+        """In-place broadcast of ``nbytes`` of a device buffer from ``root``."""
+        a = _addr(buf)
+        _check(load().ncclBroadcast(a, a, int(nbytes), NCCL_UINT8, int(root), self._comm, self._stream),
+               "ncclBroadcast")
+
+    def close(self):
+        if self._comm and self._comm.value:
+            self.ctx.sync()
+            load().ncclCommDestroy(self._comm)
+            self._comm = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except RcclError:
+        return False
+
+
+__all__ = ["Comm", "RcclError", "available", "load", "unique_id", "version"]

@@ -112,6 +112,14 @@ class DeviceArray:
         _lib.check(self.ctx._L.lslam_h2d(self.ctx.handle, self.ptr, arr.ctypes.data_as(C.c_void_p),
                                          self.nbytes), "lslam_h2d")
 
+    def download_async(self, out):
+        """D2H on the context stream without waiting: ``out`` (a C-contiguous host array of
+        the same size, ideally page-locked) holds the data after the next ``ctx.sync()``."""
+        if not (isinstance(out, np.ndarray) and out.flags.c_contiguous and out.nbytes == self.nbytes):
+            raise ValueError("download_async needs a C-contiguous host array of %d bytes" % self.nbytes)
+        _lib.check(self.ctx._L.lslam_d2h(self.ctx.handle, out.ctypes.data_as(C.c_void_p), self.ptr, self.nbytes),
+                   "lslam_d2h")
+
     def download(self, out=None):
         if out is None:
             out = np.empty(self.shape, self.dtype)

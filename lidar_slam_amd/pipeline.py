@@ -70,21 +70,22 @@ class ScanPipeline:
         self.S, self.C, self.P, self.T = S, Cn, P, int(max_trials)
         self.sco, self.cpo = sco, cpo
         self._keep = []
+        self.inputs = {}  # name -> DeviceArray of the uploaded inputs (upload_async refreshes them)
         d = self._dev
         b = _lib.ScanBatch()
         b.n_scans, b.n_chunks, b.n_points = S, Cn, P
         b.max_chunk_points = int(sizes.max()) if Cn else 0
         b.max_scan_chunks = int(per_scan.max()) if S else 0
         if polar:
-            b.theta_deg = d(theta_deg[:P] if P else np.zeros(1))
-            b.dist_mm = d(dist_mm[:P] if P else np.zeros(1))
+            b.theta_deg = d(theta_deg[:P] if P else np.zeros(1), "theta_deg")
+            b.dist_mm = d(dist_mm[:P] if P else np.zeros(1), "dist_mm")
         elif dev_xy is not None:
             self._keep.append(dev_xy)
             b.xy = dev_xy.addr
         else:
-            b.xy = d(xy[:P] if P else np.zeros((1, 2)))
-        b.scan_chunk_off = d(sco)
-        b.chunk_pt_off = d(cpo)
+            b.xy = d(xy[:P] if P else np.zeros((1, 2)), "xy")
+        b.scan_chunk_off = d(sco, "scan_chunk_off")
+        b.chunk_pt_off = d(cpo, "chunk_pt_off")
         self.hyp = HYP[hyp]
         if self.hyp == _lib.HYP_MT19937:
             if isinstance(mt_state, DeviceArray):  # a device-resident chain, e.g. another call's mt_state_out
@@ -95,7 +96,7 @@ class ScanPipeline:
             elif mt_state is not None:
                 b.mt_state_in = d(np.ascontiguousarray(mt_state, np.uint32).reshape(S, 625))
             else:
-                b.seeds = d(np.ascontiguousarray(seeds if seeds is not None else np.arange(S), np.uint32))
+                b.seeds = d(np.ascontiguousarray(seeds if seeds is not None else np.arange(S), np.uint32), "seeds")
             if want_state:
                 self.state_out = ctx.empty((S, 625), np.uint32)
                 b.mt_state_out = self.state_out.addr
@@ -145,15 +146,17 @@ class ScanPipeline:
             self.ukf_x = ctx.to_device(self.ukf_x0)
             self.ukf_P = ctx.to_device(self.ukf_P0)
             b.ukf_x, b.ukf_P = self.ukf_x.addr, self.ukf_P.addr
-            b.ukf_u = d(np.ascontiguousarray(ukf["u"], np.float64).reshape(S, 2))
-            b.ukf_z = d(np.ascontiguousarray(ukf["z"], np.float64).reshape(S, 2 * L))
-            b.ukf_lmk = d(np.ascontiguousarray(ukf["lmk"], np.float64).reshape(S, L, 2))
-            b.ukf_R_diag = d(np.ascontiguousarray(ukf["R_diag"], np.float64).reshape(2 * L))
+            b.ukf_u = d(np.ascontiguousarray(ukf["u"], np.float64).reshape(S, 2), "ukf_u")
+            b.ukf_z = d(np.ascontiguousarray(ukf["z"], np.float64).reshape(S, 2 * L), "ukf_z")
+            b.ukf_lmk = d(np.ascontiguousarray(ukf["lmk"], np.float64).reshape(S, L, 2), "ukf_lmk")
+            b.ukf_R_diag = d(np.ascontiguousarray(ukf["R_diag"], np.float64).reshape(2 * L), "ukf_R_diag")
         self.batch = b
 
-    def _dev(self, arr):
+    def _dev(self, arr, name=None):
         a = self.ctx.to_device(arr)
         self._keep.append(a)
+        if name:
+            self.inputs[name] = a
         return a.addr
 
     def reset_state(self):
@@ -164,6 +167,23 @@ class ScanPipeline:
         if self.up is not None:
             self.ukf_x.upload(self.ukf_x0)
             self.ukf_P.upload(self.ukf_P0)
+
+    def upload_async(self, **arrays):
+        """Refresh inputs on the device without a host sync (a new batch of the same shape):
+        xy / theta_deg / dist_mm / seeds / ukf_u / ukf_z / ukf_lmk by name, and ukf_x / ukf_P
+        (the filters' start state).  The host arrays must stay alive and unchanged until the
+        next sync; page-locked ones (device.register_host) copy at PCIe rate."""
+        for k, v in arrays.items():
+            dst = {"ukf_x": getattr(self, "ukf_x", None), "ukf_P": getattr(self, "ukf_P", None)}.get(k) or \
+                self.inputs.get(k)
+            if dst is None:
+                raise KeyError("no device input %r" % k)
+            dst.upload_async(np.ascontiguousarray(v, dst.dtype).reshape(dst.shape))
+
+    def clear_lists_async(self):
+        """Empty every scan's landmark list on the device (lmk_count = 0), no host sync."""
+        if self.assoc:
+            self.lmk_count.fill_zero()
 
     def run(self, sync=True):
         L = _lib.load()
@@ -231,7 +251,7 @@ def hyp_mt19937(ctx: Context, scan_chunk_off, chunk_pt_off, seeds=None, mt_state
     if mt_state is not None:
         b.mt_state_in = d(np.ascontiguousarray(mt_state, np.uint32).reshape(S, 625))
     else:
-        b.seeds = d(np.ascontiguousarray(seeds if seeds is not None else np.arange(S), np.uint32))
+        b.seeds = d(np.ascontiguousarray(seeds if seeds is not None else np.arange(S), np.uint32), "seeds")
     draws = ctx.empty((max(Cn, 1), max_trials + 1, 2), np.int32)
     st = ctx.empty((S, 625), np.uint32)
     b.draws_out, b.mt_state_out = draws.addr, st.addr

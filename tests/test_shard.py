@@ -1,0 +1,114 @@
+"""The C4 split / gather bookkeeping (lidar_slam_amd/shard.py) on CPU: a batch split
+across ranks, each rank's results gathered to the root in rank order, equals the
+single-process run bit for bit.  world_size 2 over gloo (127.0.0.1); the per-rank
+compute is the CPU oracle (this checks the partition and the gather, which the
+RCCL path shares: lidar_slam_amd/collective.py supplies the GPU transport)."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from lidar_slam_amd import shard
+from lidar_slam_amd.pipeline import LANDMARK_DTYPE, MODEL_DTYPE
+
+
+def test_shard_ranges_cover_and_balance():
+    for n, w in ((65536, 8), (10, 3), (3, 4), (0, 2), (7, 1)):
+        rs = [shard.shard_range(n, w, r) for r in range(w)]
+        assert rs[0][0] == 0 and rs[-1][1] == n
+        assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+        sizes = [hi - lo for lo, hi in rs]
+        assert max(sizes) - min(sizes) <= 1
+    assert shard.shard_range(65536, 8, 3) == (24576, 32768)
+
+
+def test_plan_inputs_rebase():
+    import bench
+    ids = list(range(7))
+    b, ukf = bench.make_workload(ids, 720, 4)
+    batch = dict(b, seeds=np.array(ids, np.uint32), **{"ukf_" + k: v for k, v in ukf.items() if k != "n_landmarks"})
+    plan = shard.plan(b["scan_chunk_off"], b["chunk_pt_off"], 3)
+    for sh in plan:
+        sub = sh.inputs(batch)
+        ref, ukr = bench.make_workload(ids[sh.lo:sh.hi], 720, 4)
+        assert np.array_equal(sub["xy"], ref["xy"])
+        assert np.array_equal(sub["scan_chunk_off"], ref["scan_chunk_off"])
+        assert np.array_equal(sub["chunk_pt_off"], ref["chunk_pt_off"])
+        assert np.array_equal(sub["seeds"], np.array(ids[sh.lo:sh.hi], np.uint32))
+        assert np.array_equal(sub["ukf_x"], batch["ukf_x"][sh.lo:sh.hi])
+        assert np.array_equal(sub["ukf_R_diag"], batch["ukf_R_diag"])  # not per scan
+
+
+def _oracle_results(b, ids, ukf, cap):
+    from oracle import cpu as orc
+    from oracle import ukf as oukf
+    mask, _, models, lists = orc.run_batch(b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], ids)
+    m = np.zeros(len(models), MODEL_DTYPE)
+    for i, d in enumerate(models):
+        for f in MODEL_DTYPE.names:
+            m[f][i] = d[f]
+    lm = np.zeros((len(ids), cap), LANDMARK_DTYPE)
+    cnt = np.zeros(len(ids), np.int32)
+    for s, lst in enumerate(lists):
+        cnt[s] = len(lst)
+        for i, L in enumerate(lst):
+            lm[s, i] = (L["a"], L["b"], L["pos"][0], L["pos"][1], L["end"][0], L["end"][1], L["id"], L["life"])
+    x, P = oukf.ukf_batch(ukf["x"], ukf["P"], ukf["u"], ukf["z"], ukf["lmk"], ukf["R_diag"])
+    return {"mask": mask, "models": m, "ukf_x": x, "ukf_P": P, "lmk_count": cnt, "landmarks": lm}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_gatherv(dist, rank):
+    def gatherv(send, recv, counts, root):
+        mine = np.ascontiguousarray(send).view(np.uint8).ravel()[:counts[rank]].tobytes()
+        objs = [None] * dist.get_world_size() if rank == root else None
+        dist.gather_object(mine, objs, dst=root)
+        if rank == root:
+            recv[:] = np.frombuffer(b"".join(objs), np.uint8)
+    return gatherv
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = list(range(5))           # ragged over 2 ranks: 3 + 2 scans
+    cap = 16
+    b, ukf = bench.make_workload(ids, 720, 6)
+    batch = dict(b, **{"ukf_" + k: v for k, v in ukf.items() if k != "n_landmarks"})
+    plan = shard.plan(b["scan_chunk_off"], b["chunk_pt_off"], world)
+    me = plan[rank]
+    sub = me.inputs(batch)
+    my_ids = ids[me.lo:me.hi]
+    uk = {k: sub["ukf_" + k] for k in ("x", "P", "u", "z", "lmk", "R_diag")}
+    local = _oracle_results(sub, my_ids, uk, cap)
+    got = shard.gather(plan, rank, local, _gloo_gatherv(dist, rank), lambda f, n: np.zeros(n, np.uint8),
+                       lmk_capacity=cap)
+    if rank == 0:
+        out["got"] = {k: shard.host_view(k, v, len(ids), cap).tobytes() for k, v in got.items()}
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_split_gather_equals_single_run():
+    import bench
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    ids = list(range(5))
+    b, ukf = bench.make_workload(ids, 720, 6)
+    ref = _oracle_results(b, ids, ukf, 16)
+    got = out["got"]
+    assert set(got) == set(shard.FIELDS)
+    for k in shard.FIELDS:
+        assert got[k] == np.ascontiguousarray(ref[k]).tobytes(), k
