@@ -13,8 +13,8 @@ seeded per scan: results identical to the reference), landmark association
 L = 20 landmarks (dim_z = 40).  One step = one pass over the batch = one launch
 of lslam_scan_pipeline.  Inputs are resident in HBM before timing.  Multi-GPU:
 each rank owns its own 4096 scans (ids rank*4096 ...), no data-path
-collective; torch.distributed (gloo) is used only for the barrier and the
-max-over-ranks of the elapsed time.
+collective; a host TCP group (lidar_slam_amd/hostgroup.py; no torch in the
+process) gives the barrier and the max-over-ranks of the elapsed time.
 
 C4 leg (configs[3]; at N > 1 by default, or --c4): one host batch of 65,536
 scans in shared memory split across the ranks, H2D + pipeline + RCCL gather of
@@ -166,13 +166,9 @@ def timed_region(step, steps, warmup, sync, barrier):
     return time.perf_counter() - t0
 
 
-def reduce_max(x, dist):
-    if dist is None:
-        return float(x)
-    import torch
-    t = torch.tensor([float(x)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def reduce_max(x, group):
+    """Max over ranks (group: lidar_slam_amd.hostgroup.HostGroup, None at one rank)."""
+    return float(x) if group is None else group.allreduce_max(float(x))
 
 
 def load_traffic(path):
@@ -214,15 +210,15 @@ def c4_leg(args, rank, world, dist, ctx, L):
         nb = int(np.prod(shape)) * np.dtype(dt).itemsize
         layout[name] = (off, shape, dt)
         off = (off + nb + 4095) & ~4095
-    seg_name = ["lslam_c4_%d_%d" % (os.getpid(), int(time.time()))]
+    seg_name = "lslam_c4_%d_%d" % (os.getpid(), int(time.time()))
     shm = None
     try:
         if rank == 0:
-            shm = shared_memory.SharedMemory(name=seg_name[0], create=True, size=off)
+            shm = shared_memory.SharedMemory(name=seg_name, create=True, size=off)
         if dist is not None:
-            dist.broadcast_object_list(seg_name, 0)
+            seg_name = dist.broadcast(seg_name.encode()).decode()
             if rank != 0:
-                shm = shared_memory.SharedMemory(name=seg_name[0])
+                shm = shared_memory.SharedMemory(name=seg_name)
         return _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan)
     finally:
         if dist is not None:
@@ -373,10 +369,10 @@ def main():
 
     dist = None
     if world > 1:
-        import datetime
-
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+        # the ranks' barrier / max-reduce over TCP (lidar_slam_amd.hostgroup): no torch in this
+        # process, whose bundled HIP runtime would sit beside /opt/rocm's and break RCCL
+        from lidar_slam_amd.hostgroup import HostGroup
+        dist = HostGroup(rank, world)
 
     from lidar_slam_amd import _lib
     from lidar_slam_amd.device import Context
@@ -389,18 +385,8 @@ def main():
     pipe = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
                         max_trials=args.trials, hyp=args.hyp, lmk_capacity=args.lmk_capacity, want_yproj=True,
                         ukf=None if args.no_ukf else ukf)
-    try:
-        import torch
-        have_torch_cuda = torch.cuda.is_available()
-        if have_torch_cuda:
-            torch.cuda.set_device(local)
-    except Exception:
-        torch, have_torch_cuda = None, False
-
     def sync_all():
         ctx.sync()
-        if have_torch_cuda:
-            torch.cuda.synchronize()
 
     def barrier():
         if dist is not None:
@@ -519,7 +505,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        dist.barrier()
+        dist.close()
     if overflows:
         sys.exit("capacity_overflows = %d: raise --lmk-capacity (the timed step was not reference-exact)"
                  % overflows)

@@ -3,8 +3,8 @@ results to the root, plus the bootstrap and a broadcast.
 
 ctypes on ROCm's librccl (rccl.h: ncclGetUniqueId :187, ncclCommInitRank :220,
 ncclBroadcast :591, ncclSend :700, ncclRecv :722, ncclGroupStart/End :923-933).
-One process per GPU; the 128-byte unique id travels over the host process group
-(gloo).  Every collective is enqueued on the lslam context's main stream
+One process per GPU; the 128-byte unique id travels over the host group
+(lidar_slam_amd/hostgroup.py).  Every collective is enqueued on the lslam context's main stream
 (lslam_ctx_stream), so it runs after the pipeline call that wrote its buffers and
 before the context's later calls, with no host sync.
 
@@ -17,6 +17,7 @@ equal, but the CSR layout allows ragged shards, which plain ncclGather does not.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 from .device import DeviceArray
 
@@ -28,7 +29,7 @@ class RcclError(RuntimeError):
 
 
 class UniqueId(C.Structure):
-    _fields_ = [("internal", C.c_char * 128)]
+    _fields_ = [("internal", C.c_ubyte * 128)]  # bytes, not a C string: it holds NULs
 
 
 _rccl = None
@@ -38,6 +39,8 @@ def load():
     global _rccl
     if _rccl is not None:
         return _rccl
+    # RCCL's diagnostics default to stdout, where bench.py prints its one JSON line
+    os.environ.setdefault("NCCL_DEBUG_FILE", "/dev/stderr")
     err = None
     for name in ("librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so"):
         try:
@@ -78,7 +81,7 @@ def version():
 def unique_id() -> bytes:
     uid = UniqueId()
     _check(load().ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
-    return bytes(bytearray(uid.internal))
+    return C.string_at(C.addressof(uid), 128)
 
 
 def _addr(x, off=0):
@@ -99,18 +102,13 @@ class Comm:
         _check(L.ncclCommInitRank(C.byref(self._comm), self.world, u, self.rank), "ncclCommInitRank")
 
     @classmethod
-    def from_process_group(cls, ctx, dist=None):
-        """Bootstrap over torch.distributed (gloo): rank 0's unique id broadcast to all."""
-        world = dist.get_world_size() if dist is not None else 1
-        rank = dist.get_rank() if dist is not None else 0
-        if world == 1:
+    def from_process_group(cls, ctx, group=None):
+        """Bootstrap over a host group (lidar_slam_amd.hostgroup.HostGroup; None = one rank):
+        rank 0's unique id broadcast to all."""
+        if group is None or group.world == 1:
             return cls(ctx, 1, 0, unique_id())
-        import torch
-        buf = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            buf[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
-        dist.broadcast(buf, 0)
-        return cls(ctx, world, rank, bytes(buf.numpy().tobytes()))
+        uid = group.broadcast(unique_id() if group.rank == 0 else None)
+        return cls(ctx, group.world, group.rank, uid)
 
     @property
     def _stream(self):

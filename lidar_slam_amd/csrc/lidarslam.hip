@@ -1990,7 +1990,11 @@ int lslam_d2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
 
 int lslam_host_register(void *p, size_t n) {
     if (!p || !n) return LSLAM_ERR_ARG;
-    HIPCHK(hipHostRegister(p, n, hipHostRegisterDefault));
+    const hipError_t e = hipHostRegister(p, n, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // not sticky: the caller falls back to pageable copies
+        return set_err(LSLAM_ERR_HIP, hipGetErrorString(e));
+    }
     return LSLAM_OK;
 }
 

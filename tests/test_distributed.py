@@ -1,13 +1,14 @@
-"""The multi-rank bench path on CPU (gloo, world_size 2, 127.0.0.1): scan
-sharding is a disjoint cover, the timed region is barrier-bracketed, and the
-elapsed time is the max over ranks.  The per-rank work here is the CPU oracle
-on each rank's shard, and the union of the shards' results equals the
-single-process run (the path has no exchange step, so none is tested)."""
+"""The multi-rank bench path on CPU (world_size 2, 127.0.0.1): scan sharding is a disjoint
+cover, the timed region is barrier-bracketed, and the elapsed time is the max over ranks.
+The ranks talk through bench.py's host group (lidar_slam_amd/hostgroup.py: TCP, no torch
+in the rank processes).  The per-rank work here is the CPU oracle on each rank's shard,
+and the union of the shards' results equals the single-process run (the main line has
+no exchange step; the C4 gather is tested in tests/test_shard.py)."""
+import multiprocessing as mp
 import os
 import socket
 
 import numpy as np
-import torch.multiprocessing as mp
 
 
 def _free_port():
@@ -20,12 +21,11 @@ def _free_port():
 
 def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch.distributed as dist
-
     import bench
     from lidar_slam_amd import synth
+    from lidar_slam_amd.hostgroup import HostGroup
     from oracle import cpu as orc
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = HostGroup.from_env()
     ids = bench.shard_scan_ids(rank, 3)
     b = synth.make_batch(ids)
     res = {}
@@ -33,22 +33,32 @@ def _worker(rank, world, port, out):
     def step():
         res["mask"] = orc.run_batch(b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], ids)[0]
 
-    el = bench.timed_region(step, 2, 1, lambda: None, dist.barrier)
+    el = bench.timed_region(step, 2, 1, lambda: None, g.barrier)
     # rank 1 pretends to be slower: the reported time must be the max
-    el_max = bench.reduce_max(el + (5.0 if rank == 1 else 0.0), dist)
-    out[rank] = (ids, res["mask"].tobytes(), el_max)
-    dist.destroy_process_group()
+    el_max = bench.reduce_max(el + (5.0 if rank == 1 else 0.0), g)
+    word = g.broadcast(b"from rank 0" if rank == 0 else None)
+    out[rank] = (ids, res["mask"].tobytes(), el_max, word)
+    g.barrier()
+    g.close()
 
 
-def test_two_rank_gloo_sharding():
+def test_two_rank_sharding_barrier_and_max():
     world = 2
-    mgr = mp.Manager()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    ids0, m0, e0 = out[0]
-    ids1, m1, e1 = out[1]
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    ids0, m0, e0, w0 = out[0]
+    ids1, m1, e1, w1 = out[1]
     assert set(ids0).isdisjoint(ids1) and sorted(ids0 + ids1) == list(range(6))
     assert e0 == e1 and e0 >= 5.0
+    assert w0 == w1 == b"from rank 0"
     from lidar_slam_amd import synth
     from oracle import cpu as orc
     b = synth.make_batch(list(range(6)))

@@ -7,7 +7,6 @@ import os
 import socket
 
 import numpy as np
-import torch.multiprocessing as mp
 
 from lidar_slam_amd import shard
 from lidar_slam_amd.pipeline import LANDMARK_DTYPE, MODEL_DTYPE
@@ -100,6 +99,8 @@ def _worker(rank, world, port, out):
 
 
 def test_two_rank_gloo_split_gather_equals_single_run():
+    import torch.multiprocessing as mp  # CPU-only test: torch stays out of GPU test sessions
+
     import bench
     world = 2
     mgr = mp.Manager()
