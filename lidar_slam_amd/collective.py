@@ -78,9 +78,25 @@ def version():
     return v.value
 
 
+class _stdout_to_stderr:
+    """RCCL prints its version banner (NCCL_DEBUG=VERSION) on fd 1 at its first call;
+    bench.py's stdout carries exactly one JSON line, so fd 1 points at fd 2 meanwhile."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def unique_id() -> bytes:
     uid = UniqueId()
-    _check(load().ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+    with _stdout_to_stderr():
+        _check(load().ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
     return C.string_at(C.addressof(uid), 128)
 
 
@@ -99,7 +115,8 @@ class Comm:
         C.memmove(C.addressof(u), uid, 128)
         self._comm = C.c_void_p()
         ctx.sync()  # ncclCommInitRank binds the calling thread's current device: the context's
-        _check(L.ncclCommInitRank(C.byref(self._comm), self.world, u, self.rank), "ncclCommInitRank")
+        with _stdout_to_stderr():
+            _check(L.ncclCommInitRank(C.byref(self._comm), self.world, u, self.rank), "ncclCommInitRank")
 
     @classmethod
     def from_process_group(cls, ctx, group=None):

@@ -237,7 +237,7 @@ def hyp_mt19937(ctx: Context, scan_chunk_off, chunk_pt_off, seeds=None, mt_state
     S, Cn = len(sco) - 1, int(sco[-1])
     keep = []
 
-    def d(a):
+    def d(a, name=None):
         x = ctx.to_device(a)
         keep.append(x)
         return x.addr
