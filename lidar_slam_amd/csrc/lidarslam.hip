@@ -298,9 +298,114 @@ __device__ __forceinline__ double tie_bound_r(double S, int N, double E2, double
     return ((double)N * (E2 + R * (sqrt(E2) + 1.0)) + (double)(N + 32) * S) * 0x1p-42;
 }
 
-__device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *cnt,
-                                    int32_t *tied, double *tsum, int32_t *inl, double *vtmp, double *vstack,
-                                    int *nstack, int32_t *cnt_out, int lane) {
+// The count pass reads the chunk's points with scalar loads (through the
+// scalar cache, into SGPRs) when the batch holds Cartesian xy: every lane (a
+// hypothesis) uses the same point, which then is an FP64 SGPR operand of its
+// FMAs.  The LDS-broadcast form of the same loop is bound by the LDS return
+// path (1 KiB per point and wave) and by its load latency.  Scalar loads can
+// return out of order, so their wait is lgkmcnt(0): the loop issues the next
+// group's load right AFTER waiting for the current one, and the current
+// group's arithmetic covers the latency.  The loads are inline asm (the
+// compiler would wait for the prefetch before the current group); the waits
+// are asm statements that the loaded values pass through.
+typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x16 sload_4pts(const double2 *p) {
+    u32x16 v;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u32x4 sload_pt(const double2 *p) {
+    u32x4 v;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void swait(u32x16 &v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)::"memory"); }
+__device__ __forceinline__ void swait(u32x4 &v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)::"memory"); }
+__device__ __forceinline__ double sd(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// one point against the lane's hypothesis: r = fl(x uy - fl(y ux + k)),
+// S += r^2, lo += |r| <= r_lo, hi += |r| < r_hi
+__device__ __forceinline__ void count_one(double x, double y, double ux, double uy, double k, double r_lo,
+                                          double r_hi, int &lo, int &hi, double &S) {
+    const double r = __builtin_fma(x, uy, -__builtin_fma(y, ux, k));
+    S = __builtin_fma(r, r, S);
+    lo += (fabs(r) <= r_lo) ? 1 : 0;
+    hi += (fabs(r) < r_hi) ? 1 : 0;
+    asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
+}
+
+// one hypothesis per lane against all N points (gP: global, wave-uniform)
+__device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, double ux, double uy, double k,
+                                                  double r_lo, double r_hi, int &lo, int &hi, double &S) {
+    int p = 0;
+    if (N >= 4) {
+        // two SGPR buffers in turn, so no copies between the load and its use
+        u32x16 A = sload_4pts(gP), B;
+        for (;;) {
+            swait(A);
+            const bool moreB = p + 8 <= N;
+            if (moreB) B = sload_4pts(gP + p + 4);
+            count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            p += 4;
+            if (!moreB) break;
+            swait(B);
+            const bool moreA = p + 8 <= N;
+            if (moreA) A = sload_4pts(gP + p + 4);
+            count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_one(sd(B[12], B[13]), sd(B[14], B[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            p += 4;
+            if (!moreA) break;
+        }
+    }
+    for (; p < N; p++) {
+        u32x4 v = sload_pt(gP + p);
+        swait(v);
+        count_one(sd(v[0], v[1]), sd(v[2], v[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+    }
+}
+
+// the same from the LDS copy (polar batches: points converted on load)
+__device__ __forceinline__ void count_points_lds(const double2 *P, int N, double ux, double uy, double k, double r_lo,
+                                                 double r_hi, int &lo, int &hi, double &S) {
+    int p = 0;
+    for (; p + 2 <= N; p += 2) {
+        const double2 q0 = P[p], q1 = P[p + 1];
+        count_one(q0.x, q0.y, ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(q1.x, q1.y, ux, uy, k, r_lo, r_hi, lo, hi, S);
+    }
+    if (p < N) count_one(P[p].x, P[p].y, ux, uy, k, r_lo, r_hi, lo, hi, S);
+}
+
+// diagnostic build only: chunk_kernel phase cycles into dbg[c][k] (k < 8)
+#ifdef LSLAM_STAMPS
+#define CH_STAMP(k)                                                            \
+    do {                                                                       \
+        const uint64_t _t = lslam_stamp();                                     \
+        if (chdbg && lane == 0) chdbg[(k)] += _t - _ch_prev;                   \
+        _ch_prev = _t;                                                         \
+    } while (0)
+#define CH_STAMP_DECL uint64_t _ch_prev = lslam_stamp();
+#define CH_STAMP_DECL_RESET _ch_prev = lslam_stamp();
+#else
+#define CH_STAMP_DECL_RESET
+#define CH_STAMP(k) do {} while (0)
+#define CH_STAMP_DECL
+#endif
+
+__device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const double2 *gP, int N, const int32_t *draws,
+                                    int32_t *cnt, int32_t *tied, double *tsum, int32_t *inl, double *vtmp,
+                                    double *vstack, int *nstack, int32_t *cnt_out, int lane,
+                                    unsigned long long *chdbg = nullptr) {
+    CH_STAMP_DECL
     const int T = a.T;
     const double ecut = a.ecut;
     double xmn = __builtin_inf(), xmx = -__builtin_inf(), ymn = __builtin_inf(), ymx = -__builtin_inf();
@@ -341,6 +446,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
     const double margin = (E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
     const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
     int M = 0;
+    CH_STAMP(1);
     for (int tb = 0; tb < T; tb += 64) {
         const int t = tb + lane;
         const int tt = t < T ? t : 0;
@@ -350,23 +456,8 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         const double k = __builtin_fma(m.ox, m.uy, -(m.oy * m.ux));
         int lo = 0, hi = 0;
         double S = 0.0;
-        int p = 0;
-        for (; p + 2 <= N; p += 2) {
-            const double2 q0 = P[p], q1 = P[p + 1];
-            const double r0 = __builtin_fma(q0.x, m.uy, -__builtin_fma(q0.y, m.ux, k));
-            const double r1 = __builtin_fma(q1.x, m.uy, -__builtin_fma(q1.y, m.ux, k));
-            S = __builtin_fma(r0, r0, S);
-            S = __builtin_fma(r1, r1, S);
-            lo += (int)(fabs(r0) <= r_lo) + (int)(fabs(r1) <= r_lo);
-            hi += (int)(fabs(r0) < r_hi) + (int)(fabs(r1) < r_hi);
-        }
-        if (p < N) {
-            const double2 q = P[p];
-            const double r = __builtin_fma(q.x, m.uy, -__builtin_fma(q.y, m.ux, k));
-            S = __builtin_fma(r, r, S);
-            lo += (int)(fabs(r) <= r_lo);
-            hi += (int)(fabs(r) < r_hi);
-        }
+        if (gP) count_points_sgpr(gP, N, m.ux, m.uy, k, r_lo, r_hi, lo, hi, S);
+        else count_points_lds(P, N, m.ux, m.uy, k, r_lo, r_hi, lo, hi, S);
         int c = lo;
         if (exact_all || lo != hi) {  // rare: lane-divergent exact recount
             c = 0;
@@ -386,6 +477,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
         M = max(M, wave_max(t < T ? c : 0));
     }
     M = uni(M);
+    CH_STAMP(2);
     __syncthreads();
     // compact the max-count trials in trial order
     int ntied = 0;
@@ -454,7 +546,10 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, int N, con
             }
         }
     }
-    return chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    CH_STAMP(3);
+    const ChunkOut of = chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    CH_STAMP(4);
+    return of;
 }
 
 // mask (LDS copy + global) and A8 line parameters (ransac_functions.py:25-31)
@@ -1209,6 +1304,12 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
+#ifdef LSLAM_STAMPS
+    unsigned long long *chdbg = a.dbg ? a.dbg + (size_t)c * 16 : nullptr;
+#else
+    unsigned long long *chdbg = nullptr;
+#endif
+    CH_STAMP_DECL
     lslam_chunk_model rec;
     memset(&rec, 0, sizeof(rec));
     rec.best_trial = -1;
@@ -1236,16 +1337,21 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
     }
+    CH_STAMP(0);
     stage_points(B, p0, N, P, lane);
     __syncthreads();
-    const ChunkOut o = chunk_consensus(a, P, N, draws, cnt, tied, tsum, inl, vtmp, vstack, nstack,
-                                       B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
+    CH_STAMP(6);
+    const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
+    const ChunkOut o = chunk_consensus(a, P, gP, N, draws, cnt, tied, tsum, inl, vtmp, vstack, nstack,
+                                       B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane, chdbg);
+    CH_STAMP_DECL_RESET
     const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
     if (B.y_proj && a.write_yproj) {
         const double pa = rec.proj_a, pb = rec.proj_b;
         for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
     }
     if (lane == 0 && B.models) B.models[c] = rec;
+    CH_STAMP(5);
 }
 
 template <int HYP>
