@@ -1,6 +1,8 @@
-"""Summarise rocprofv3 outputs of tools/run_gpu.sh into profiles/.
+"""Summarise a tools/profile_session.sh run into profiles/.
 
-  python tools/profile_summary.py <tag>   (reads gpurun_out/, writes profiles/<tag>_*)
+  python tools/profile_summary.py <tag> [bench_log]
+      reads gpurun_out/prof_<tag>/{kt,fetch,write,sq1,sq2} and the bench line of the
+      same build (default gpurun_out/bench.log); writes profiles/<tag>_*
 
 Kernel time comes from --kernel-trace --stats; HBM traffic from separate
 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (MI355X_MICROARCH.md §HBM:
@@ -37,14 +39,15 @@ KERNELS = {"rng_kernel": "rng_kernel", "resolve_kernel": "resolve_kernel", "chun
            "post": "scan_kernel<2, "}
 
 
-def main(tag):
+def main(tag, bench_log=None):
     os.makedirs(PROF, exist_ok=True)
-    stats = rows(os.path.join(OUT, "prof_kt", "kt_kernel_stats.csv"))
-    bench = [json.loads(l) for l in open(os.path.join(OUT, "bench.json")) if l.startswith("{")][-1]
+    S = os.path.join(OUT, "prof_" + tag)
+    stats = rows(os.path.join(S, "kt", "kt_kernel_stats.csv"))
+    bench = [json.loads(l) for l in open(bench_log or os.path.join(OUT, "bench.log")) if l.startswith("{")][-1]
     per = {}
     for k, sub in KERNELS.items():
-        fetch = counter(os.path.join(OUT, "prof_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", sub)
-        write = counter(os.path.join(OUT, "prof_write", "write_counter_collection.csv"), "WRITE_SIZE", sub)
+        fetch = counter(os.path.join(S, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE", sub)
+        write = counter(os.path.join(S, "write", "write_counter_collection.csv"), "WRITE_SIZE", sub)
         if not fetch or not write:
             continue
         f_kib = sum(fetch) / len(fetch)
@@ -64,7 +67,25 @@ def main(tag):
         lines.append("- `%s`: FETCH_SIZE %.1f KiB, WRITE_SIZE %.1f KiB -> %d bytes/launch"
                      % (k, v["fetch_kib"], v["write_kib"], v["bytes_per_launch"]))
     # the profiled process's own bench line: its HIP-event kernel time must agree with rocprof's
-    prof_line = [l for l in open(os.path.join(OUT, "prof_kt.log")) if l.startswith('{"metric"')]
+    scans = bench["config"]["scans_per_gpu"]
+    sq = {}
+    for p in ("sq1", "sq2"):
+        f = os.path.join(S, p, p + "_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for k, sub in KERNELS.items():
+            names = {r["Counter_Name"] for r in rows(f)}
+            for n in sorted(names):
+                v = counter(f, n, sub)
+                if v:
+                    sq.setdefault(k, {})[n] = sum(v) / len(v)
+    if sq:
+        lines += ["", "SQ counters per launch (separate --pmc passes), and per scan (%d scans):" % scans, "",
+                  "| kernel | counter | per launch | per scan |", "|---|---|---|---|"]
+        for k, d in sq.items():
+            for n, v in d.items():
+                lines.append("| `%s` | %s | %.4g | %.4g |" % (k, n, v, v / scans))
+    prof_line = [l for l in open(os.path.join(S, "kt.log")) if l.startswith('{"metric"')]
     if prof_line:
         pb = json.loads(prof_line[-1])
         roc = [float(r["AverageNs"]) / 1e3 for r in stats if "rng_kernel" in r["Name"]]
@@ -74,14 +95,15 @@ def main(tag):
                      100.0 * ((roc[0] if roc else 0) / (1e3 * pb["roofline"]["kernel_ms"]) - 1.0), pb["ms_per_step"])]
     lines += ["", "bench.py line of the same build (separate run, no profiler):", "", "```", json.dumps(bench), "```"]
     open(os.path.join(PROF, "%s_rocprof.md" % tag), "w").write("\n".join(lines) + "\n")
-    for src in ("prof_kt/kt_kernel_stats.csv",):
-        data = open(os.path.join(OUT, src)).read()
+    for src in ("kt/kt_kernel_stats.csv",):
+        data = open(os.path.join(S, src)).read()
         open(os.path.join(PROF, "%s_%s" % (tag, os.path.basename(src))), "w").write(data)
-    t = {"tag": tag, "scans": bench["config"]["scans_per_gpu"], "hyp": bench["config"]["hyp"], "kernels": per}
+    t = {"tag": tag, "scans": scans, "hyp": bench["config"]["hyp"], "kernels": per,
+         "sq_per_scan": {k: {n: v / scans for n, v in d.items()} for k, d in sq.items()}}
     json.dump(t, open(os.path.join(PROF, "traffic_latest.json"), "w"), indent=1)
     json.dump(bench, open(os.path.join(PROF, "%s_bench.json" % tag), "w"))
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
