@@ -33,6 +33,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/lidarslam.h"
 #include "lslam_express.h"
@@ -111,8 +112,9 @@ struct KArgs {
     int res_g;          // resolve_kernel: LDS staging capacity (bytes)
     int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
     uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
-    int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
+    int off_blk, off_fl, off_nxt, off_vtmp, off_stage, off_tbl;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
+    const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127 (null: mask evaluation only)
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
@@ -1080,6 +1082,8 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         unsigned char *base = smem + (size_t)j * a.rng_pipe_bytes;
         rp.blk = (uint32_t *)(base + a.off_blk);
         rp.fl = (lds_flag_t *)(base + a.off_fl);
+        rp.tbl = (uint32_t *)(base + a.off_tbl);
+        rp.tblK = 0;
         return rp;
     };
     if (wave < PPW) {
@@ -1121,7 +1125,10 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
             const int N = B.chunk_pt_off[c + 1] - p0;
             if (N < 3) continue;
             JT *Jc = J + (size_t)D * (size_t)p0;
-            if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            if (a.rt_all && (uint32_t)N - 1u <= RT_KMAX) {
+                if (rp.tblK != (uint32_t)N - 1u) rt_load(rp, a.rt_all, (uint32_t)N - 1u, lane);
+                parse_chunk_tbl(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            } else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
             else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
         }
         lds_flag_put(rp.fl + F_BLKUSE, -1);  // this pipe needs no more blocks
@@ -1258,7 +1265,7 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
             if ((uint32_t)lane < nd) {
                 const JT *trow = tile + lane * STRIDE;
                 for (uint32_t i = i0; i < i1; i++) {
-                    const uint32_t j = trow[K - i - mlo];
+                    const uint32_t j = trow[K - i - mlo] & step_mask(i);
                     c0 = (j == c0) ? i : c0;
                     c1 = (j == c1) ? i : c1;
                 }
@@ -1267,7 +1274,7 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
         }
         if ((uint32_t)lane < nd) {
             const uint32_t d = d0 + (uint32_t)lane;
-            const uint32_t j1 = Jc[(size_t)lane * K + (K - 1u)];
+            const uint32_t j1 = Jc[(size_t)lane * K + (K - 1u)] & 1u;
             int32_t *draws = a.draws_scr + (size_t)c * 2 * D;
             draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
             draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
@@ -1834,6 +1841,8 @@ struct lslam_ctx {
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
     int rng_ppw;
+    // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h); null = off
+    uint32_t *rt_all;
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
@@ -1869,6 +1878,19 @@ struct lslam_ctx {
 };
 
 static thread_local std::string g_err;
+
+// rows v = 0..127 of every K = 2..127, built once per process (rt_word, lslam_rng_pipe.h)
+static const std::vector<uint32_t> &reject_tables() {
+    static const std::vector<uint32_t> t = [] {
+        std::vector<uint32_t> v((size_t)(RT_KMAX - 1) * RT_DWORDS);
+        for (uint32_t K = 2; K <= RT_KMAX; K++)
+            for (uint32_t r = 0; r < (uint32_t)RT_ROWS; r++)
+                for (uint32_t q = 0; q < (uint32_t)RT_ST; q++)
+                    v[(size_t)(K - 2) * RT_DWORDS + r * RT_ST + q] = rt_word(K, r, q);
+        return v;
+    }();
+    return t;
+}
 
 static int set_err(int code, const char *msg) {
     g_err = msg;
@@ -1934,6 +1956,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
     if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
+    c->rt_all = nullptr;
     if (const char *e = getenv("LSLAM_CONSUMER_WGS")) {
         const int v = atoi(e);
         if (v > 0) c->consumer_wgs = v;
@@ -1980,6 +2003,14 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     HIPCHK(hipEventRecord(c->ev_slot_free[1], c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     HIPCHK(hipEventRecord(c->ev_call, c->stream));
+    {
+        const char *e = getenv("LSLAM_RNG_TABLE");  // 0: mask evaluation only (A/B)
+        if (!e || atoi(e) != 0) {
+            const std::vector<uint32_t> &t = reject_tables();
+            HIPCHK(hipMalloc(&c->rt_all, t.size() * 4));
+            HIPCHK(hipMemcpy(c->rt_all, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
     *out = c;
     return LSLAM_OK;
 }
@@ -2000,6 +2031,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     if (c->cscr) (void)hipFree(c->cscr);
     for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
+    if (c->rt_all) (void)hipFree(c->rt_all);
     hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
@@ -2461,6 +2493,7 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
     int off = 0;
     k.off_blk = off; off += align16(2 * 4 * 624);
     k.off_fl = off; off += align16(4 * F_NFLAGS);
+    k.off_tbl = off; off += (N - 1 <= (int)RT_KMAX) ? align16(4 * RT_DWORDS) : 0;
     k.rng_pipe_bytes = off;
     lds = off * ppw;
     return LSLAM_OK;
@@ -2566,6 +2599,7 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
 
 static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
+    k.rt_all = c->rt_all;
     int lds = 0;
     const int ppw = c->rng_ppw;
     int st = layout_rng(k, &k.b, lds, ppw);

@@ -89,9 +89,38 @@ __device__ __forceinline__ void mt_twist_oop(const uint32_t *src, uint32_t *dst,
     wave_lds_sync();
 }
 
+// ---------------- reject tables (chunks of at most 128 points) ----------------
+// For K = N-1 <= 127 a word's fate depends on w only through v = w & mask(K)
+// (<= 127), and on its step only through x = (step of the window's first
+// word within its draw) + (words accepted before it in the window).  Row v of
+// the table for K holds, bit x, whether random_interval rejects v at
+// i = K - (x mod K): (v & mask(i)) > i.  A window of 64 words then needs, per
+// lane, the 64 bits x in [sg, sg+63] of its row (3 dwords + 2 funnel shifts),
+// and one fixed-point iteration is v_mbcnt x2, a 64-bit shift and a compare
+// (the reject bit of the lane's current count), not the 9-op mask evaluation.
+// x runs over at most K-1 + 63 + 32 < 224 bits: 7 dwords per row (odd, so the
+// lanes' random rows spread over the LDS banks).
+constexpr uint32_t RT_KMAX = 127;
+constexpr int RT_ROWS = 128;
+constexpr int RT_ST = 7;
+constexpr int RT_DWORDS = RT_ROWS * RT_ST;  // one K's table: 3.5 KiB
+__host__ __device__ inline uint32_t rt_word(uint32_t K, uint32_t v, uint32_t q) {
+    uint32_t word = 0;
+    for (uint32_t b = 0; b < 32; b++) {
+        const uint32_t x = q * 32u + b;
+        const uint32_t i = K - x % K;
+        uint32_t m = i;
+        m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+        if ((v & m) > i) word |= 1u << b;
+    }
+    return word;
+}
+
 struct RngPipe {
     uint32_t *blk;         // LDS [2][624] raw MT state, block b in slot b & 1
     lds_flag_t *fl;        // LDS [F_NFLAGS]
+    uint32_t *tbl;         // LDS [RT_ROWS][RT_ST]: reject table of the current K
+    uint32_t tblK;         // K of the table in tbl (0 = none)
     uint32_t total_steps;  // parser: steps of the whole scan (priority schedule)
     uint32_t done_steps;   // parser: steps of the finished chunks
     int prio;              // parser: current priority level
@@ -283,6 +312,154 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
     rp.done_steps += G;
 }
 
+// ---------------- parser wave, table mode (K <= 127) ----------------
+// Lane l of a window holds word pos+l; a_l = accepted words below it, and
+// s_l = 63 - a_l = v_mbcnt(reject ballot, 63 - l).  Bit a of the lane's 64-bit
+// window M (x = sg + a) is its reject flag at that count, i.e. bit 63 of
+// M << s.  Accepted lanes store v at step g + a_l; the consumer applies
+// mask(i) itself (v & mask(i) = the step's j), so no per-lane i is formed here.
+// random_interval's mask for step index i >= 1 (wave-uniform i: scalar ops)
+__device__ __forceinline__ uint32_t step_mask(uint32_t i) { return 0xffffffffu >> __clz((int)i); }
+
+__device__ __forceinline__ bool rt_rej(uint64_t M, uint32_t s) { return (int32_t)(uint32_t)((M << s) >> 32) < 0; }
+
+// (sg + na) mod K for sg < K, na <= 64: one conditional subtraction when K >= 64
+__device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
+    x = min(x, x - K);  // unsigned: x - K wraps high when x < K
+    if (K < 64)
+        while (x >= K) x -= K;
+    return x;
+}
+
+// tempered word & mask(K): the two xor-with-masked-shift steps as v_bitop3 ((a & b) ^ c)
+__device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
+    y ^= (y >> 11);
+    y = __builtin_amdgcn_bitop3_b32(y << 7, 0x9d2c5680u, y, 0x6a);
+    y = __builtin_amdgcn_bitop3_b32(y << 15, 0xefc60000u, y, 0x6a);
+    return (y ^ (y >> 18)) & mK;
+}
+
+__device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
+    const uint32_t *row = tbl + v * RT_ST + (sg >> 5);
+    const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
+    const uint32_t r = sg & 31u;
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, r);
+    const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, r);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// the table for K from the library's global copy (rt_all[K-2]) into the pipe
+__device__ __forceinline__ void rt_load(RngPipe &rp, const uint32_t *__restrict__ rt_all, uint32_t K, int lane) {
+    const uint32_t mK = 0xffffffffu >> __clz((int)K);
+    const uint4 *src = (const uint4 *)(rt_all + (size_t)(K - 2u) * RT_DWORDS);
+    uint4 *dst = (uint4 *)rp.tbl;
+    const uint32_t n4 = (mK + 1u) * RT_ST / 4u;  // rows 0..mK (mK + 1 >= 4, a power of two)
+    for (uint32_t e = (uint32_t)lane; e < n4; e += 64) dst[e] = src[e];
+    wave_lds_sync();
+    rp.tblK = K;
+}
+
+template <typename JT>
+__device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &pos, JT *__restrict__ J, uint32_t N,
+                                                uint32_t D, int lane) {
+    const uint32_t K = N - 1;
+    const uint32_t G = D * K;
+    const uint32_t mK = 0xffffffffu >> __clz((int)K);
+    const uint32_t sbase = 63u - (uint32_t)lane;
+    const uint32_t s0 = 63u - (((uint32_t)lane * 46u) >> 6);  // ~0.72 accepts per word below the lane
+    uint32_t g = 0, sg = 0;
+    int pre_pos = -1;
+    uint32_t pre_raw = 0;
+    RP_STAMP_DECL
+    while (g < G) {
+        RP_STAMP(3);
+        if (pos >= MT_N) {
+            blkno += 1;
+            while (lds_flag_get(rp.fl + F_BLK) < blkno) __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+            pos = 0;
+            pre_pos = -1;
+            lds_flag_put(rp.fl + F_BLKUSE, blkno);
+            wake_helper();
+            const int lvl = RP_PRIO_TOP - (int)(((uint64_t)(rp.done_steps + g) * 3u) / (rp.total_steps + 1u));
+            if (lvl != rp.prio) {
+                rp.prio = lvl;
+                set_prio_level(lvl);
+            }
+            RP_STAMP(0);
+        }
+        const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
+        const uint32_t rem = G - g;
+        // a run of full windows: inside this block and short of the chunk's end
+        const int nrun = min((MT_N - pos) >> 6, (int)((rem - 1u) >> 6));
+        if (nrun > 0) {
+            uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
+            for (int r = 0; r < nrun; r++) {
+                // next window's words: past the block's end this reads the rest of the pipe's LDS; never used
+                const uint32_t nraw = kb[pos + 64 + lane];
+                const uint32_t v = rt_temper_mask(raw, mK);
+                const uint64_t M = rt_window(rp.tbl, v, sg);
+                RP_STAMP(3);
+                // three evaluations without a convergence check (one more evaluation of
+                // the fixed point leaves it unchanged; ~5 are needed on average), then
+                // one per check: fewer VALU -> SALU round trips and branches
+                uint64_t R = ballot(rt_rej(M, s0));
+#pragma unroll
+                for (int e = 0; e < 3; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
+                uint32_t s;
+                int it = 4;
+                for (;;) {
+                    s = mbcnt_from(R, sbase);
+                    const uint64_t Rn = ballot(rt_rej(M, s));
+                    it++;
+                    if (Rn == R) break;
+                    R = Rn;
+                }
+                (void)it;
+                RP_STAMP(2);
+                RP_COUNT(5, 1);
+                RP_COUNT(6, it);
+                store_accepted(J, (g + 63u) - s, v, R);
+                const uint32_t na = accepted_count(R);
+                pos += 64;
+                g += na;
+                sg = rt_wrap(sg + na, K);
+                raw = nraw;
+            }
+            pre_pos = pos;
+            pre_raw = raw;
+            continue;
+        }
+        // ---- partial window: block end or chunk end.  A = accept ballot (active
+        // lanes whose count is below rem); ~A counts every other lane as rejected.
+        const uint32_t raw = (pre_pos == pos) ? pre_raw : kb[min(pos + lane, MT_N - 1)];
+        pre_pos = -1;
+        const uint32_t v = rt_temper_mask(raw, mK);
+        const uint64_t M = rt_window(rp.tbl, v, sg);
+        RP_STAMP(3);
+        const int nw = min(64, MT_N - pos);
+        const uint64_t actm = ballot(lane < nw);
+        const int thr = 63 - (int)min(rem, 64u);  // a < rem  <=>  s > thr
+        uint64_t A = actm & ballot(!rt_rej(M, s0) && (int)s0 > thr);
+        uint32_t s;
+        for (;;) {
+            s = mbcnt_from(~A, sbase);
+            const uint64_t An = actm & ballot(!rt_rej(M, s) && (int)s > thr);
+            if (An == A) break;
+            A = An;
+        }
+        RP_STAMP(2);
+        RP_COUNT(5, 1);
+        if ((A >> lane) & 1ull) J[(g + 63u) - s] = (JT)v;
+        const uint32_t na = (uint32_t)popc64(A);
+        if (na >= rem && na > 0) pos += fls64(A) + 1;
+        else pos += nw;
+        g += na;
+        sg = rt_wrap(sg + na, K);
+    }
+    rp.done_steps += G;
+}
+
 // ---------------- helper wave: keeps the next MT block ready ----------------
 __device__ __forceinline__ void rng_helper(const RngPipe &rp, int lane) {
     int produced = 0;
@@ -300,8 +477,9 @@ __device__ __forceinline__ void rng_helper(const RngPipe &rp, int lane) {
 }
 
 // ---------------- resolution: steps -> draws, one wave per chunk ----------------
-// Lanes are draws.  For draw d, step s has i = K - s and j_i = J[d*K + s]
-// (j_i <= i).  Fisher-Yates swaps x[i] and x[j_i] for i = K..1, so a forward
+// Lanes are draws.  For draw d, step s has i = K - s and j_i = J[d*K + s] &
+// mask(i) (j_i <= i; the table-mode parser stores w & mask(K), the other the
+// masked j itself, and masking again leaves it unchanged).  Fisher-Yates swaps x[i] and x[j_i] for i = K..1, so a forward
 // scan over i = 2..K recovers where the values that START at positions 0 and 1
 // of the last step's input come from: p <- i whenever j_i == p (the value at p
 // was swapped there by step i, and no later, smaller-i step writes position
@@ -319,7 +497,7 @@ __device__ __forceinline__ void resolve_draws_fwd(const JT *__restrict__ Js, uin
     for (; i + 8 <= K + 1; i += 8) {
         uint32_t jj[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) jj[u] = Jd[K - i - u];
+        for (int u = 0; u < 8; u++) jj[u] = Jd[K - i - u] & step_mask(i + u);
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             c0 = (jj[u] == c0) ? i + u : c0;
@@ -327,12 +505,12 @@ __device__ __forceinline__ void resolve_draws_fwd(const JT *__restrict__ Js, uin
         }
     }
     for (; i <= K; i++) {
-        const uint32_t j = Jd[K - i];
+        const uint32_t j = Jd[K - i] & step_mask(i);
         c0 = (j == c0) ? i : c0;
         c1 = (j == c1) ? i : c1;
     }
     if (live) {
-        const uint32_t j1 = Jd[K - 1];
+        const uint32_t j1 = Jd[K - 1] & 1u;
         draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
         draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
     }
