@@ -82,6 +82,21 @@ __device__ __forceinline__ void stage_points(const lslam_scan_batch &B, int p0, 
 }
 static_assert(sizeof(lslam_landmark) == 56, "landmark ABI");
 
+// owning scan of chunk c: the last s with scan_chunk_off[s] <= c.  Batches of
+// equal scans (C3: 8 chunks each) hit the proportional guess with one load
+// pair; otherwise a binary search (a chain of dependent loads).
+__device__ __forceinline__ int owning_scan(const lslam_scan_batch &B, int c) {
+    const int g = (int)(((int64_t)c * B.n_scans) / (B.n_chunks > 0 ? B.n_chunks : 1));
+    if (g < B.n_scans && B.scan_chunk_off[g] <= c && c < B.scan_chunk_off[g + 1]) return uni(g);
+    int lo = 0, hi = B.n_scans;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (B.scan_chunk_off[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    return uni(lo);
+}
+
 enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8, MODE_POST = 16 };
 
 // ------------------------------------------------------------------------
@@ -410,25 +425,28 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
     CH_STAMP_DECL
     const int T = a.T;
     const double ecut = a.ecut;
+    // bounding box and finiteness in one pass; the four reductions interleaved
     double xmn = __builtin_inf(), xmx = -__builtin_inf(), ymn = __builtin_inf(), ymx = -__builtin_inf();
+    bool finite = true;
     for (int p = lane; p < N; p += 64) {
         const double2 q = P[p];
         xmn = fmin(xmn, q.x);
         xmx = fmax(xmx, q.x);
         ymn = fmin(ymn, q.y);
         ymx = fmax(ymx, q.y);
-    }
-    xmn = wave_min_d(xmn);
-    xmx = wave_max_d(xmx);
-    ymn = wave_min_d(ymn);
-    ymx = wave_max_d(ymx);
-    const double bx = xmx - xmn, by = ymx - ymn;
-    const double E2 = unid((bx * bx + by * by) * (1.0 + 0x1p-20));
-    bool finite = E2 < __builtin_inf();
-    for (int p = lane; p < N; p += 64) {
-        const double2 q = P[p];
         finite = finite && (q.x - q.x == 0.0) && (q.y - q.y == 0.0);
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a0 = __shfl_xor(xmn, o), a1 = __shfl_xor(xmx, o), a2 = __shfl_xor(ymn, o), a3 = __shfl_xor(ymx, o);
+        xmn = fmin(xmn, a0);
+        xmx = fmax(xmx, a1);
+        ymn = fmin(ymn, a2);
+        ymx = fmax(ymx, a3);
+    }
+    const double bx = xmx - xmn, by = ymx - ymn;
+    const double E2 = unid((bx * bx + by * by) * (1.0 + 0x1p-20));
+    finite = finite && E2 < __builtin_inf();
     if (N > 128 || ballot(!finite) != 0ull || !(ecut < __builtin_inf()))
         return chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack, cnt_out, lane);
 
@@ -1300,14 +1318,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     int *nstack = (int *)(smem + a.off_nstack);
     double *vtmp = (double *)(smem + a.off_vtmp);
 
-    // owning scan: the last s with scan_chunk_off[s] <= c
-    int lo = 0, hi = B.n_scans;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (B.scan_chunk_off[mid] <= c) lo = mid;
-        else hi = mid;
-    }
-    const int s = uni(lo);
+    const int s = owning_scan(B, c);
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
@@ -1626,13 +1637,7 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
     double *vst = (double *)(smem + a.off_vstack);
     int *nstack = (int *)(smem + a.off_nstack);
     double *vtmp = (double *)(smem + a.off_vtmp);
-    int lo = 0, hi = B.n_scans;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (B.scan_chunk_off[mid] <= c) lo = mid;
-        else hi = mid;
-    }
-    const int s = uni(lo);
+    const int s = owning_scan(B, c);
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T, D = T + 1;
@@ -2329,7 +2334,7 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         // default "033": resolve and consensus (the chain the next producer waits on) issue
         // ahead of the parsers' lower levels; the long post pass stays below them
         const char *e = getenv("LSLAM_CONS_PRIO");
-        if (!e || strlen(e) != 3) e = "033";
+        if (!e || strlen(e) != 3) e = "000";
         return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4);
     }();
     k.cons_prio = cons_prio;
@@ -2814,7 +2819,8 @@ static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
         set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
     const dim3 grid(launch_cap(c, k.b.n_scans));
-    if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
+    static const bool w4 = [] { const char *e = getenv("LSLAM_POST_W4"); return e && atoi(e) != 0; }();
+    if (k.hyp_source == LSLAM_HYP_MT19937 && !w4)  // beside the next call's producer
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     else
         hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
