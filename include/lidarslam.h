@@ -256,6 +256,11 @@ int lslam_set_timing(lslam_ctx *ctx, int enable);
 int lslam_set_timing_mask(lslam_ctx *ctx, uint32_t mask);
 int lslam_timing(lslam_ctx *ctx, int kernel, double *total_ms, int64_t *launches);  /* syncs */
 int lslam_timing_reset(lslam_ctx *ctx);
+/* Bytes of Fisher-Yates steps scratch per producer slot (two slots; default 2 GiB, or the
+ * LSLAM_STEPS_BUDGET environment variable).  A parity-mode call whose scans are one chunk each
+ * (C5) and whose steps exceed it runs the producer in epochs of as many draws as fit, each
+ * resolved before its slot is reused.  bytes <= 0 restores the default.  Syncs. */
+int lslam_set_steps_budget(lslam_ctx *ctx, int64_t bytes);
 
 /* ---- host helpers ---- */
 int lslam_ransac_params_default(lslam_ransac_params *p);

@@ -90,7 +90,7 @@ EXPORTS = [
     "lslam_ctx_destroy", "lslam_sync", "lslam_malloc", "lslam_free", "lslam_host_alloc", "lslam_host_free",
     "lslam_h2d", "lslam_d2h", "lslam_d2d", "lslam_memset", "lslam_host_register", "lslam_host_unregister",
     "lslam_ctx_stream", "lslam_abi_sizes", "lslam_set_timing", "lslam_set_timing_mask", "lslam_timing",
-    "lslam_timing_reset",
+    "lslam_timing_reset", "lslam_set_steps_budget",
     "lslam_ransac_params_default", "lslam_ukf_params_default", "lslam_inlier_cutoff", "lslam_ukf_weights",
     "lslam_mt_seed_state", "lslam_polar_to_xy", "lslam_hyp_mt19937", "lslam_ransac", "lslam_landmarks",
     "lslam_ukf_step", "lslam_scan_pipeline", "lslam_express_decode", "lslam_express_scans",
@@ -142,6 +142,7 @@ def load():
         "lslam_set_timing_mask": ([_VP, u32], C.c_int),
         "lslam_timing": ([_VP, C.c_int, P(dbl), P(i64)], C.c_int),
         "lslam_timing_reset": ([_VP], C.c_int),
+        "lslam_set_steps_budget": ([_VP, i64], C.c_int),
         "lslam_ransac_params_default": ([P(RansacParams)], C.c_int),
         "lslam_ukf_params_default": ([P(UkfParams), i32], C.c_int),
         "lslam_inlier_cutoff": ([dbl], dbl),

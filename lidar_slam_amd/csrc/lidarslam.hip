@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <new>
@@ -130,6 +131,11 @@ struct KArgs {
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage, off_tbl;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127 (null: mask evaluation only)
+    // producer epochs (one-chunk scans whose steps exceed the slot budget): this launch
+    // covers draws [ep_d0, ep_d0 + ep_nd) of every chunk; ep_nd = 0: all T + 1 draws
+    int ep_d0, ep_nd;
+    int ep_count;        // host: producer launches of the call
+    size_t slot_jbytes;  // host: steps bytes of a slot (its MT state area follows)
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
@@ -1094,7 +1100,7 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
     const int lane = (int)threadIdx.x & 63;
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
-    const uint32_t D = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : (uint32_t)a.T + 1u;  // draws of this launch
     auto pipe_of = [&](int j) {
         RngPipe rp;
         unsigned char *base = smem + (size_t)j * a.rng_pipe_bytes;
@@ -1215,14 +1221,15 @@ __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
-    const uint32_t D = (uint32_t)a.T + 1u;
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
     if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
         if (N >= 3)
             resolve_chunk((const JT *)a.jbuf + (size_t)D * (size_t)p0, (uint32_t)N - 1u, D, (uint32_t)a.res_g, smem,
-                          a.draws_scr + (size_t)c * 2 * D, lane);
+                          a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)a.ep_d0, lane);
         __syncthreads();
     }
 }
@@ -1243,7 +1250,8 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
     JT *tile = (JT *)smem;
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
-    const uint32_t D = (uint32_t)a.T + 1u;
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
     if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     const int64_t total = (int64_t)B.n_chunks * ngroups;
     for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
@@ -1293,7 +1301,7 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
         if ((uint32_t)lane < nd) {
             const uint32_t d = d0 + (uint32_t)lane;
             const uint32_t j1 = Jc[(size_t)lane * K + (K - 1u)] & 1u;
-            int32_t *draws = a.draws_scr + (size_t)c * 2 * D;
+            int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)a.ep_d0;
             draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
             draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
         }
@@ -1848,6 +1856,7 @@ struct lslam_ctx {
     int rng_ppw;
     // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h); null = off
     uint32_t *rt_all;
+    size_t steps_budget;  // producer slot budget (prepare_steps)
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
@@ -1883,6 +1892,12 @@ struct lslam_ctx {
 };
 
 static thread_local std::string g_err;
+
+static size_t default_steps_budget() {
+    const char *e = getenv("LSLAM_STEPS_BUDGET");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (size_t)v : ((size_t)2 << 30);
+}
 
 // rows v = 0..127 of every K = 2..127, built once per process (rt_word, lslam_rng_pipe.h)
 static const std::vector<uint32_t> &reject_tables() {
@@ -1962,6 +1977,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->rng_ppw = 4;
     if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
     c->rt_all = nullptr;
+    c->steps_budget = default_steps_budget();
     if (const char *e = getenv("LSLAM_CONSUMER_WGS")) {
         const int v = atoi(e);
         if (v > 0) c->consumer_wgs = v;
@@ -2537,11 +2553,25 @@ static void set_max_lds(F *fn) {
 // D * chunk_pt_off[c]; + slack for 16-byte staging loads) and the end-of-scan
 // MT state.  The resolved draws live in the main-stream scratch unless the
 // caller asked for draws_out.
+// Epochs: when every scan is one chunk (C5) and the steps of all T + 1 draws
+// exceed the slot budget (LSLAM_STEPS_BUDGET bytes, default 2 GiB), the producer
+// runs in launches of ep_nd draws, each resolved before its slot is reused; the
+// MT state chains through the slots' state areas.  k.ep_count launches.
 static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     const int N = k.b.max_chunk_points;
     k.j8 = N <= 256 ? 1 : 0;
-    const size_t jbytes = ((size_t)(k.T + 1) * (size_t)(k.b.n_points > 0 ? k.b.n_points : 1) * (k.j8 ? 1 : 2)
-                           + 64 + 255) & ~(size_t)255;
+    const size_t per_draw = (size_t)(k.b.n_points > 0 ? k.b.n_points : 1) * (k.j8 ? 1 : 2);
+    const size_t budget = c->steps_budget;
+    const int D = k.T + 1;
+    int De = D;
+    if (k.b.max_scan_chunks == 1 && (size_t)D * per_draw > budget) {
+        const size_t fit = budget / per_draw;
+        De = fit < 1 ? 1 : (fit < (size_t)D ? (int)fit : D);
+    }
+    k.ep_nd = De < D ? De : 0;
+    k.ep_d0 = 0;
+    k.ep_count = (D + De - 1) / De;
+    const size_t jbytes = ((size_t)De * per_draw + 64 + 255) & ~(size_t)255;
     const size_t sbytes = (size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4;
     if (c->pslot_bytes < jbytes + sbytes) {
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -2560,6 +2590,7 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     }
     k.jbuf = c->pslot[slot];
     k.state_scr = (uint32_t *)((unsigned char *)c->pslot[slot] + jbytes);
+    k.slot_jbytes = jbytes;
     if (k.b.draws_out) {
         k.draws_scr = k.b.draws_out;
     } else {
@@ -2577,11 +2608,12 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     const int N = k.b.max_chunk_points > 3 ? k.b.max_chunk_points : 3;
     const int esz = k.j8 ? 1 : 2;
     // stage a chunk's steps in LDS when they fit 16 KiB (C3: 101 x 99 B), else stream them from HBM
-    const int64_t need = ((int64_t)(k.T + 1) * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
+    const int De = k.ep_nd > 0 ? k.ep_nd : k.T + 1;  // draws of this launch
+    const int64_t need = ((int64_t)De * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
     const int lds = need <= 16 * 1024 ? (int)need : 0;
     k.res_g = lds;  // staging capacity in bytes
     if (lds == 0) {  // steps streamed through LDS tiles, waves over (chunk, 64 draws)
-        const int ngroups = (k.T + 1 + 63) / 64;
+        const int ngroups = (De + 63) / 64;
         const int64_t items = (int64_t)k.b.n_chunks * ngroups;
         const dim3 grid(launch_cap(c, items > (1 << 30) ? (1 << 30) : items)), block(64);
         const int tl = 64 * (RB + 4) * esz;
@@ -2628,6 +2660,54 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     }
     HIPCHK(hipGetLastError());
     return timer_end(c, LSLAM_K_RNG, stream);
+}
+
+// Producer + resolve of a call: one launch, or k.ep_count epochs in alternating
+// slots (prepare_steps).  rng_kernel runs on `ps` (after the previous epoch's
+// resolve released its slot), the resolve on the ctx stream.  final_out: where
+// the last launch writes the end state (null: the slot's state area).  On return
+// k.state_scr is the end state's area and last_slot the slot the caller releases.
+static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint32_t *final_out, int &last_slot) {
+    const int D = k.T + 1;
+    // Epochs run on the ctx stream one after the other: an epoch's resolve beside the next
+    // epoch's producer slowed the parsers more than it hid (C5: 129 vs 112 ms per call)
+    if (k.ep_count > 1 && ps != c->stream) {
+        HIPCHK(hipEventRecord(c->ev_produced, ps));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
+        ps = c->stream;
+    }
+    const uint32_t *prev_state = nullptr;
+    int sl = slot;
+    for (int e = 0; e < k.ep_count; e++) {
+        KArgs ke = k;
+        if (k.ep_count > 1) {
+            ke.ep_d0 = e * k.ep_nd;
+            ke.ep_nd = std::min(k.ep_nd, D - ke.ep_d0);
+            ke.jbuf = c->pslot[sl];
+            ke.state_scr = (uint32_t *)((unsigned char *)c->pslot[sl] + k.slot_jbytes);
+            if (e > 0) {
+                if (ps != c->stream) HIPCHK(hipStreamWaitEvent(ps, c->ev_slot_free[sl], 0));
+                ke.b.mt_state_in = prev_state;  // the previous epoch's end state (same parser, draw boundary)
+            }
+        }
+        const bool last = e == k.ep_count - 1;
+        ke.b.mt_state_out = (last && final_out) ? final_out : ke.state_scr;
+        int st = launch_rng(c, ke, ps);
+        if (st) return st;
+        if (ps != c->stream) {
+            HIPCHK(hipEventRecord(c->ev_produced, ps));
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
+        }
+        st = launch_resolve(c, ke);
+        if (st) return st;
+        if (!last) HIPCHK(hipEventRecord(c->ev_slot_free[sl], c->stream));
+        prev_state = ke.state_scr;
+        last_slot = sl;
+        sl ^= 1;
+    }
+    k.state_scr = const_cast<uint32_t *>(prev_state);
+    c->next_slot = sl;
+    return LSLAM_OK;
 }
 
 static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
@@ -2839,7 +2919,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     int st = build_args(k, b, p, nullptr, MODE_RANSAC, lds_fix);
     if (st) return st;
     const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
-    const int slot = c->next_slot;
+    int slot = c->next_slot;
     if (mt) {
         st = prepare_steps(c, k, slot);
         if (st) return st;
@@ -2894,13 +2974,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
             c->out_unknown = 0;
         }
         if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
-        KArgs kr = k;
-        kr.b.mt_state_out = k.state_scr;
-        st = launch_rng(c, kr, c->pstream);
-        if (st) return st;
-        HIPCHK(hipEventRecord(c->ev_produced, c->pstream));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
-        st = launch_resolve(c, k);
+        st = produce_draws(c, k, slot, c->pstream, nullptr, slot);  // slot <- the last epoch's
         if (st) return st;
     }
     st = launch_chunks(c, k, !assoc);
@@ -2976,6 +3050,15 @@ int lslam_polar_to_xy(lslam_ctx *c, const double *th, const double *d, double *x
     return end_call(c);
 }
 
+int lslam_set_steps_budget(lslam_ctx *c, int64_t bytes) {
+    if (!c) return LSLAM_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->pstream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->steps_budget = bytes > 0 ? (size_t)bytes : default_steps_budget();
+    return LSLAM_OK;
+}
+
 int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trials) {
     if (!c) return LSLAM_ERR_ARG;
     int st = validate_batch(b, false);
@@ -2998,17 +3081,17 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     st = timer_begin(c, LSLAM_K_HYP);
     if (st) return st;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_slot_free[slot], 0));
-    st = launch_rng(c, k, c->stream);  // on the main stream; the end state goes straight to mt_state_out
+    int last = slot;
+    // on the main stream; the end state goes straight to mt_state_out
+    st = produce_draws(c, k, slot, c->stream, b->mt_state_out, last);
     if (st) return st;
-    st = launch_resolve(c, k);
-    if (st) return st;
-    HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+    HIPCHK(hipEventRecord(c->ev_slot_free[last], c->stream));
     // the end state is written by the rng kernel itself, final at ev_slot_free[slot]: a
     // pipeline call chaining from it waits for that event, anything else for ev_call
     note_out(c, b->draws_out, (size_t)b->n_chunks * 2 * (size_t)(max_trials + 1) * 4);
     note_out(c, b->mt_state_out, (size_t)b->n_scans * 625 * 4);
     c->prev_state_out = b->mt_state_out;
-    c->prev_slot = slot;
+    c->prev_slot = last;
     c->prev_fixed = b->mt_state_out ? 1 : 0;
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_HYP);

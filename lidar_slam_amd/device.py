@@ -46,6 +46,11 @@ class Context:
     def timing_reset(self):
         _lib.check(self._L.lslam_timing_reset(self.handle), "lslam_timing_reset")
 
+    def set_steps_budget(self, nbytes: int = 0):
+        """Producer steps scratch per slot (bytes; 0 = default 2 GiB).  One-chunk scans whose
+        parity-mode steps exceed it run the producer in epochs (lslam_set_steps_budget)."""
+        _lib.check(self._L.lslam_set_steps_budget(self.handle, int(nbytes)), "lslam_set_steps_budget")
+
     @property
     def stream(self):
         """The context's main hipStream_t (int address), for collectives enqueued after its calls."""

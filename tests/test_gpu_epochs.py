@@ -1,0 +1,95 @@
+"""GPU: the parity producer in epochs (lslam_set_steps_budget).
+
+One-chunk scans whose Fisher-Yates steps exceed the slot budget run the MT19937
+producer in launches of as many draws as fit, each resolved before its slot is
+reused, the stream state chained between launches (C5: 68.7 GB of steps per call
+otherwise).  The draws, the end state and every pipeline output must equal the
+single-launch run byte for byte, and the oracle's choice(N, 2) sequence.
+Reference semantics: fit.py:819-826 (numpy legacy choice on the global stream).
+"""
+import numpy as np
+import pytest
+
+from oracle import cpu as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from lidar_slam_amd.device import Context
+    if Context.device_count() < 1:
+        pytest.skip("no HIP device")
+    c = Context(0)
+    yield c
+    c.set_steps_budget(0)
+
+
+def _one_chunk_batch(n, S):
+    sco = np.arange(S + 1, dtype=np.int32)
+    cpo = (np.arange(S + 1) * n).astype(np.int32)
+    return sco, cpo
+
+
+@pytest.mark.parametrize("n,trials,budget_draws", [(100, 150, 7), (100, 100, 64), (300, 120, 13), (1000, 60, 1)])
+def test_hyp_epochs_equal_single_launch(ctx, n, trials, budget_draws):
+    """u8 (table-mode parse) and u16 steps, LDS-staged and tiled resolves, 1..64 draws per epoch."""
+    from lidar_slam_amd import pipeline as pl
+    S = 20
+    seeds = np.arange(S, dtype=np.uint32) + 500
+    sco, cpo = _one_chunk_batch(n, S)
+    ctx.set_steps_budget(0)
+    d1, s1 = pl.hyp_mt19937(ctx, sco, cpo, seeds=seeds, max_trials=trials)
+    esz = 1 if n <= 256 else 2
+    ctx.set_steps_budget(budget_draws * S * n * esz)  # budget_draws draws per epoch
+    try:
+        d2, s2 = pl.hyp_mt19937(ctx, sco, cpo, seeds=seeds, max_trials=trials)
+    finally:
+        ctx.set_steps_budget(0)
+    assert np.array_equal(d1, d2)
+    assert np.array_equal(s1, s2)
+    for s in (0, S - 1):
+        st = orc.MTState(seed=int(seeds[s]))
+        ref = np.array([st.choice2(n) for _ in range(trials + 1)])
+        assert np.array_equal(d2[s], ref)
+        assert np.array_equal(s2[s, :624], st.key) and s2[s, 624] == st.pos.value
+
+
+def test_pipeline_epochs_chained_state(ctx):
+    """The fused pipeline in epochs, from an explicit MT state, twice in a row (the second call
+    chains from the first's end state): masks, models, draws and states equal the single-launch
+    run, and the oracle."""
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import ScanPipeline
+    S, n, trials = 12, 600, 90
+    xys = [synth.polar_to_xy_ref(*synth.scan_polar(700 + s, n_beams=n, cfg=5)[:2]) for s in range(S)]
+    xy = np.concatenate(xys)
+    sco, cpo = _one_chunk_batch(n, S)
+    st0 = np.stack([np.append(orc.MTState(seed=40 + s).key, 624) for s in range(S)]).astype(np.uint32)
+
+    def two_calls():
+        p = ScanPipeline(ctx, xy, sco, cpo, mt_state=st0, max_trials=trials, want_draws=True, want_state=True)
+        p.run()
+        r1 = p.results()
+        p2 = ScanPipeline(ctx, xy, sco, cpo, mt_state=r1["mt_state"], max_trials=trials, want_draws=True,
+                          want_state=True)
+        p2.run()
+        return r1, p2.results()
+
+    ctx.set_steps_budget(0)
+    a1, a2 = two_calls()
+    ctx.set_steps_budget(5 * S * n * 2)  # 5 draws per epoch: 19 launches per call
+    try:
+        b1, b2 = two_calls()
+    finally:
+        ctx.set_steps_budget(0)
+    for ra, rb in ((a1, b1), (a2, b2)):
+        for k in ("mask", "draws", "mt_state"):
+            assert np.array_equal(ra[k], rb[k]), k
+        assert ra["models"].tobytes() == rb["models"].tobytes()
+    for s in (0, 5):
+        st = orc.MTState(seed=40 + s)
+        mo, md, _ = orc.ransac(xys[s], 20.0, trials, state=st)
+        assert np.array_equal(b1["mask"][s * n:(s + 1) * n], mo)
+        assert b1["models"]["best_trial"][s] == md["best_trial"]
+        assert np.array_equal(b1["mt_state"][s, :624], st.key)

@@ -34,8 +34,11 @@ def main():
     ap.add_argument("--landmarks", type=int, default=200)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--hyp", default="both")
+    ap.add_argument("--budget-gib", type=float, default=0.0,
+                    help="producer steps scratch per slot (0: the library default, 2 GiB)")
     args = ap.parse_args()
     ctx = Context(0)
+    ctx.set_steps_budget(int(args.budget_gib * (1 << 30)))
     S, Np, T = args.scans, args.points, args.trials
     ids = list(range(S))
     b, ukf = make_workload(ids, Np, args.landmarks)
@@ -58,7 +61,14 @@ def main():
         for name, k in (("consensus", _lib.K_CONSENSUS), ("rng", _lib.K_RNG)):
             m2, n2 = ctx.timing(k)
             if n2:
-                res[name + "_ms"] = m2 / n2
+                res[name + "_ms"] = m2 / args.reps  # per call (the producer may run in epochs)
+                res[name + "_launches_per_call"] = n2 / args.reps
+        if hyp == "mt19937":  # two slots of min(budget, all steps) bytes (u16 steps)
+            full = (T + 1) * S * Np * 2
+            budget = args.budget_gib * (1 << 30) if args.budget_gib > 0 else 2 << 30
+            per_draw = S * Np * 2
+            slot = full if full <= budget else max(1, int(budget // per_draw)) * per_draw
+            res["steps_scratch_gb"] = 2 * slot / 1e9
         ctx.set_timing(False)
         if "consensus_ms" in res:
             flops = 12.0 * Np * T * S
