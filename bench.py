@@ -346,6 +346,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg at N > 1")
     ap.add_argument("--c4-scans", type=int, default=65536, help="C4: scans of the one shared batch")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--no-alone", action="store_true", help="skip the producer-alone timing (profiled runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -411,6 +412,21 @@ def main():
     ravg = reduce_max(rms / rl, dist) if rl else None
     cavg = reduce_max(cms / max(cl, 1), dist)
 
+    # the producer alone (no consumers beside it), for the record: lslam_hyp_mt19937 over the same batch
+    alone = None
+    if args.hyp == "mt19937" and not args.no_alone:
+        from lidar_slam_amd import pipeline as pl
+        pl.hyp_mt19937(ctx, b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
+                       max_trials=args.trials)
+        ctx.set_timing(True, kernels=[_lib.K_RNG])
+        ctx.timing_reset()
+        for _ in range(3):
+            pl.hyp_mt19937(ctx, b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
+                           max_trials=args.trials)
+        ams, al = ctx.timing(_lib.K_RNG)
+        ctx.set_timing(False)
+        alone = reduce_max(ams / max(al, 1), dist)
+
     # sanity: results are well-formed (every chunk fitted or flagged)
     r = pipe.results()
     valid = int(np.sum((r["models"]["flags"] & 1) != 0))
@@ -447,6 +463,7 @@ def main():
         roof = {"bound": "valu", "achieved": round(achieved, 4), "peak": VALU_PEAK_TOPS, "unit": "TOPS (int32)",
                 "frac": round(achieved / VALU_PEAK_TOPS, 5), "traffic": traffic_of("rng_kernel"),
                 "kernel": "rng_kernel (MT19937 parse, lslam_rng_pipe.h)", "kernel_ms": round(ravg, 4),
+                "kernel_alone_ms": round(alone, 4) if alone else None,
                 "ops_per_launch": round(ops), "ops_def": "%d per MT word (expected words from random_interval's "
                 "acceptance) + %d per Fisher-Yates step" % (OPS_PER_WORD, OPS_PER_STEP)}
     else:
