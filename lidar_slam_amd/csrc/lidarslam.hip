@@ -1139,6 +1139,7 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
             const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
             if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
         }
+        rp_set_schedule(rp);
         rp.prio = RP_PRIO_TOP;
         set_prio_level(RP_PRIO_TOP);
         int blkno = 0;

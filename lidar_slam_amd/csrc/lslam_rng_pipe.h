@@ -116,18 +116,32 @@ __host__ __device__ inline uint32_t rt_word(uint32_t K, uint32_t v, uint32_t q) 
     return word;
 }
 
+struct RngPipe;
+__device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done);
+
 struct RngPipe {
     uint32_t *blk;         // LDS [2][624] raw MT state, block b in slot b & 1
     lds_flag_t *fl;        // LDS [F_NFLAGS]
     uint32_t *tbl;         // LDS [RT_ROWS][RT_ST]: reject table of the current K
     uint32_t tblK;         // K of the table in tbl (0 = none)
     uint32_t total_steps;  // parser: steps of the whole scan (priority schedule)
+    uint32_t lvl_t1, lvl_t2;  // parser: done steps at which the level drops (rp_set_schedule)
     uint32_t done_steps;   // parser: steps of the finished chunks
     int prio;              // parser: current priority level
 #ifdef LSLAM_STAMPS
     uint64_t acc[8];
 #endif
 };
+
+// Level RP_PRIO_TOP - floor(3 done / (total + 1)): two compares against thresholds set
+// once per scan instead of a 64-bit division at every block switch.
+__device__ __forceinline__ void rp_set_schedule(RngPipe &rp) {
+    rp.lvl_t1 = (rp.total_steps + 1u + 2u) / 3u;        // ceil((total + 1) / 3)
+    rp.lvl_t2 = (2u * (rp.total_steps + 1u) + 2u) / 3u;  // ceil(2 (total + 1) / 3)
+}
+__device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done) {
+    return RP_PRIO_TOP - (done >= rp.lvl_t1 ? 1 : 0) - (done >= rp.lvl_t2 ? 1 : 0);
+}
 
 // Diagnostic build only: parser cycle accounting (0 block waits, 2 fixed point,
 // 3 rest of the window, 5 windows, 6 fixed-point evaluations)
@@ -211,7 +225,7 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             pre_pos = -1;
             lds_flag_put(rp.fl + F_BLKUSE, blkno);
             wake_helper();
-            const int lvl = RP_PRIO_TOP - (int)(((uint64_t)(rp.done_steps + g) * 3u) / (rp.total_steps + 1u));
+            const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;
                 set_prio_level(lvl);
@@ -381,7 +395,7 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             pre_pos = -1;
             lds_flag_put(rp.fl + F_BLKUSE, blkno);
             wake_helper();
-            const int lvl = RP_PRIO_TOP - (int)(((uint64_t)(rp.done_steps + g) * 3u) / (rp.total_steps + 1u));
+            const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;
                 set_prio_level(lvl);
@@ -493,21 +507,27 @@ __device__ __forceinline__ void resolve_draws_fwd(const JT *__restrict__ Js, uin
     const bool live = d < D;
     const JT *Jd = Js + (size_t)(live ? d : d0) * K;
     uint32_t c0 = 0, c1 = 1;
-    uint32_t i = 2;
-    for (; i + 8 <= K + 1; i += 8) {
-        uint32_t jj[8];
+    // i = 2..K in runs of one mask class [2^b, 2^(b+1)): the mask is loop-invariant
+    for (uint32_t lo = 2; lo <= K;) {
+        const uint32_t m = step_mask(lo);
+        const uint32_t hi = min(K, m);
+        uint32_t i = lo;
+        for (; i + 8 <= hi + 1; i += 8) {
+            uint32_t jj[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) jj[u] = Jd[K - i - u] & step_mask(i + u);
+            for (int u = 0; u < 8; u++) jj[u] = Jd[K - i - u] & m;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            c0 = (jj[u] == c0) ? i + u : c0;
-            c1 = (jj[u] == c1) ? i + u : c1;
+            for (int u = 0; u < 8; u++) {
+                c0 = (jj[u] == c0) ? i + u : c0;
+                c1 = (jj[u] == c1) ? i + u : c1;
+            }
         }
-    }
-    for (; i <= K; i++) {
-        const uint32_t j = Jd[K - i] & step_mask(i);
-        c0 = (j == c0) ? i : c0;
-        c1 = (j == c1) ? i : c1;
+        for (; i <= hi; i++) {
+            const uint32_t j = Jd[K - i] & m;
+            c0 = (j == c0) ? i : c0;
+            c1 = (j == c1) ? i : c1;
+        }
+        lo = hi + 1;
     }
     if (live) {
         const uint32_t j1 = Jd[K - 1] & 1u;
