@@ -1158,6 +1158,10 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         }
         lds_flag_put(rp.fl + F_BLKUSE, -1);  // this pipe needs no more blocks
         wake_helper();
+        if (pos > MT_N) {  // the last window ran across the block end: its block is in (numpy twisted too)
+            blkno += 1;
+            pos -= MT_N;
+        }
         if (B.mt_state_out) {
             uint32_t *o = B.mt_state_out + (size_t)s * 625;
             const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
@@ -1202,6 +1206,10 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
                 live = true;
                 if (use == produced[j]) {
                     mt_twist_oop(rp.blk + (produced[j] & 1) * MT_N, rp.blk + ((produced[j] + 1) & 1) * MT_N, lane);
+                    if (((produced[j] + 1) & 1) == 0) {  // pad after slot 1 = the new block's head
+                        rp.blk[2 * MT_N + lane] = rp.blk[lane];
+                        wave_lds_sync();
+                    }
                     produced[j] += 1;
                     lds_flag_put(rp.fl + F_BLK, produced[j]);
                     busy = true;
@@ -2513,7 +2521,7 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
     const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
     int off = 0;
-    k.off_blk = off; off += align16(2 * 4 * 624);
+    k.off_blk = off; off += align16(4 * (2 * 624 + 64));  // two block slots + the head pad
     k.off_fl = off; off += align16(4 * F_NFLAGS);
     k.off_tbl = off; off += (N - 1 <= (int)RT_KMAX) ? align16(4 * RT_DWORDS) : 0;
     k.rng_pipe_bytes = off;

@@ -13,9 +13,10 @@
 //                     at D * chunk_pt_off[c] + d*K + s (u8 if every chunk has
 //                     <= 256 points, else u16).
 //   wave 1 (helper):  twists block b+1 of the MT state out of place while the
-//                     parser reads block b (two 624-word slots of raw state).
-//                     It sleeps until the parser wakes it (s_wakeup) at a
-//                     block switch.
+//                     parser reads block b (two 624-word slots of raw state,
+//                     then a 64-word pad holding slot 0's head, so a window
+//                     may run across the block boundary).  It sleeps until a
+//                     parser wakes it (s_wakeup) at a block switch (rng_kernel).
 // Turning the steps into the two drawn indices is bulk, data-parallel work
 // (resolve_chunk below); it runs in the consensus kernel, one wave per chunk,
 // where all of a chunk's draws are resolved together.
@@ -221,7 +222,7 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             blkno += 1;
             while (lds_flag_get(rp.fl + F_BLK) < blkno) __builtin_amdgcn_s_sleep(1);
             asm volatile("" ::: "memory");
-            pos = 0;
+            pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
             lds_flag_put(rp.fl + F_BLKUSE, blkno);
             wake_helper();
@@ -391,7 +392,7 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             blkno += 1;
             while (lds_flag_get(rp.fl + F_BLK) < blkno) __builtin_amdgcn_s_sleep(1);
             asm volatile("" ::: "memory");
-            pos = 0;
+            pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
             lds_flag_put(rp.fl + F_BLKUSE, blkno);
             wake_helper();
@@ -404,12 +405,19 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
         const uint32_t rem = G - g;
-        // a run of full windows: inside this block and short of the chunk's end
-        const int nrun = min((MT_N - pos) >> 6, (int)((rem - 1u) >> 6));
+        // A run of full windows short of the chunk's end, up to the block's end; the last one
+        // may run across it: the LDS holds [block slot 0][slot 1][pad = head of slot 0], so the
+        // words after the boundary follow contiguously once the helper has the next block in.
+        const int nrun = min((MT_N - pos + 63) >> 6, (int)((rem - 1u) >> 6));
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
             for (int r = 0; r < nrun; r++) {
-                // next window's words: past the block's end this reads the rest of the pipe's LDS; never used
+                if (pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
+                    while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
+                    asm volatile("" ::: "memory");
+                    raw = kb[pos + lane];
+                }
+                // next window's words (after a crossing window: discarded by the block switch)
                 const uint32_t nraw = kb[pos + 64 + lane];
                 const uint32_t v = rt_temper_mask(raw, mK);
                 const uint64_t M = rt_window(rp.tbl, v, sg);
@@ -444,15 +452,20 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             pre_raw = raw;
             continue;
         }
-        // ---- partial window: block end or chunk end.  A = accept ballot (active
-        // lanes whose count is below rem); ~A counts every other lane as rejected.
-        const uint32_t raw = (pre_pos == pos) ? pre_raw : kb[min(pos + lane, MT_N - 1)];
+        // ---- the chunk's last window (rem <= 64), possibly across the block boundary.
+        // A = accept ballot (lanes whose count is below rem); ~A counts the others as rejected.
+        if (pos + 64 > MT_N) {
+            while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+            pre_pos = -1;
+        }
+        const uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
         pre_pos = -1;
         const uint32_t v = rt_temper_mask(raw, mK);
         const uint64_t M = rt_window(rp.tbl, v, sg);
         RP_STAMP(3);
-        const int nw = min(64, MT_N - pos);
-        const uint64_t actm = ballot(lane < nw);
+        const int nw = 64;
+        const uint64_t actm = ~0ull;
         const int thr = 63 - (int)min(rem, 64u);  // a < rem  <=>  s > thr
         uint64_t A = actm & ballot(!rt_rej(M, s0) && (int)s0 > thr);
         uint32_t s;
@@ -472,22 +485,6 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         sg = rt_wrap(sg + na, K);
     }
     rp.done_steps += G;
-}
-
-// ---------------- helper wave: keeps the next MT block ready ----------------
-__device__ __forceinline__ void rng_helper(const RngPipe &rp, int lane) {
-    int produced = 0;
-    for (;;) {
-        const int use = lds_flag_get(rp.fl + F_BLKUSE);
-        if (use < 0) return;  // parser finished
-        if (use == produced) {
-            mt_twist_oop(rp.blk + (produced & 1) * MT_N, rp.blk + ((produced + 1) & 1) * MT_N, lane);
-            produced += 1;
-            lds_flag_put(rp.fl + F_BLK, produced);
-            continue;
-        }
-        __builtin_amdgcn_s_sleep(127);  // until the parser's s_wakeup
-    }
 }
 
 // ---------------- resolution: steps -> draws, one wave per chunk ----------------
