@@ -1368,12 +1368,31 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     } else {
         // explicit draws, or the parity stream's draws resolved by resolve_kernel
         const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
-        for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
+        if (2 * D <= 256 && N <= 128 && B.xy) {
+            // C3-sized chunk: the draws' and the points' loads in flight together (one memory
+            // latency instead of one per copy loop), then into LDS
+            int32_t dv[4];
+            double2 pv[2];
+            const double2 *src = (const double2 *)B.xy + p0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) dv[k] = (lane + 64 * k < 2 * D) ? h[lane + 64 * k] : 0;
+#pragma unroll
+            for (int k = 0; k < 2; k++) pv[k] = (lane + 64 * k < N) ? src[lane + 64 * k] : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (lane + 64 * k < 2 * D) draws[lane + 64 * k] = dv[k];
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                if (lane + 64 * k < N) P[lane + 64 * k] = pv[k];
+        } else {
+            for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
+            stage_points(B, p0, N, P, lane);
+        }
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
     }
     CH_STAMP(0);
-    stage_points(B, p0, N, P, lane);
+    if (HYP == LSLAM_HYP_PHILOX) stage_points(B, p0, N, P, lane);
     __syncthreads();
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
