@@ -93,3 +93,33 @@ def test_pipeline_epochs_chained_state(ctx):
         assert np.array_equal(b1["mask"][s * n:(s + 1) * n], mo)
         assert b1["models"]["best_trial"][s] == md["best_trial"]
         assert np.array_equal(b1["mt_state"][s, :624], st.key)
+
+
+@pytest.mark.parametrize("n", [20, 65, 100, 128])
+def test_table_parse_windows_across_block_ends(ctx, n):
+    """Table-mode parse (chunks of <= 128 points) from states whose position sits just before,
+    at and after the 624-word block end, and one- to three-chunk scans: draws and end states
+    (key + pos, numpy's lazy twist at pos == 624 included) equal the oracle's."""
+    from lidar_slam_amd import pipeline as pl
+    starts = [0, 100, 560, 600, 620, 623, 624]
+    S = len(starts) * 3
+    sizes, states, chunks = [], [], []
+    for k, p0 in enumerate(starts):
+        for nch in (1, 2, 3):
+            st = orc.MTState(seed=3000 + 10 * k + nch)
+            st.pos.value = p0
+            states.append(np.append(st.key, p0))
+            chunks.append(nch)
+            sizes += [n - (c % 2) for c in range(nch)]
+    sco = np.concatenate([[0], np.cumsum(chunks)]).astype(np.int32)
+    cpo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    trials = 37
+    draws, state = pl.hyp_mt19937(ctx, sco, cpo, mt_state=np.array(states, np.uint32), max_trials=trials)
+    for s in range(S):
+        st = orc.MTState(key=states[s][:624], pos=int(states[s][624]))
+        for c in range(sco[s], sco[s + 1]):
+            nc = int(cpo[c + 1] - cpo[c])
+            ref = np.array([st.choice2(nc) for _ in range(trials + 1)])
+            assert np.array_equal(draws[c], ref), (n, s, c)
+        assert np.array_equal(state[s, :624], st.key), (n, s)
+        assert state[s, 624] == st.pos.value, (n, s)
