@@ -123,3 +123,39 @@ def test_table_parse_windows_across_block_ends(ctx, n):
             assert np.array_equal(draws[c], ref), (n, s, c)
         assert np.array_equal(state[s, :624], st.key), (n, s)
         assert state[s, 624] == st.pos.value, (n, s)
+
+
+def test_epochs_with_an_early_stop(ctx):
+    """A one-chunk scan whose points are all on one line stops at the first trial (residual sum
+    exactly 0, fit.py:866-869); the fix-up replays it from the input state.  In epochs the other
+    scans' draws and end states come from the chained launches: every output equals the
+    single-launch run, and the collinear scan's end state the oracle's."""
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import ScanPipeline
+    S, n, trials = 6, 300, 80
+    xys = [synth.polar_to_xy_ref(*synth.scan_polar(900 + s, n_beams=n, cfg=5)[:2]) for s in range(S)]
+    xys[2] = np.stack([np.linspace(-900.0, 1500.0, n), np.full(n, 7.0)], 1)
+    xy = np.concatenate(xys)
+    sco, cpo = _one_chunk_batch(n, S)
+    seeds = np.arange(S) + 77
+
+    def run():
+        p = ScanPipeline(ctx, xy, sco, cpo, seeds=seeds, max_trials=trials, want_draws=True, want_state=True)
+        p.run()
+        return p.results()
+
+    ctx.set_steps_budget(0)
+    a = run()
+    ctx.set_steps_budget(9 * S * n * 2)  # 9 draws per epoch
+    try:
+        b = run()
+    finally:
+        ctx.set_steps_budget(0)
+    assert b["models"]["flags"][2] & 16 and b["models"]["n_draws"][2] < trials + 1
+    for k in ("mask", "draws", "mt_state"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["models"].tobytes() == b["models"].tobytes()
+    st = orc.MTState(seed=int(seeds[2]))
+    mo, md, _ = orc.ransac(xys[2], 20.0, trials, state=st)
+    assert np.array_equal(b["mask"][2 * n:3 * n], mo)
+    assert np.array_equal(b["mt_state"][2, :624], st.key) and b["mt_state"][2, 624] == st.pos.value
