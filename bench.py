@@ -213,12 +213,25 @@ def c4_leg(args, rank, world, dist, ctx, L):
     seg_name = "lslam_c4_%d_%d" % (os.getpid(), int(time.time()))
     shm = None
     try:
+        # every rank learns whether the segment exists on all of them before any collective
+        err = None
         if rank == 0:
-            shm = shared_memory.SharedMemory(name=seg_name, create=True, size=off)
+            try:
+                shm = shared_memory.SharedMemory(name=seg_name, create=True, size=off)
+            except Exception as e:  # e.g. /dev/shm smaller than the batch
+                err = e
         if dist is not None:
-            seg_name = dist.broadcast(seg_name.encode()).decode()
-            if rank != 0:
-                shm = shared_memory.SharedMemory(name=seg_name)
+            name = dist.broadcast((seg_name if err is None else "").encode()).decode()
+            if rank != 0 and name:
+                try:
+                    shm = shared_memory.SharedMemory(name=name)
+                except Exception as e:
+                    err = e
+            failed = dist.allreduce_max(0.0 if (name and err is None) else 1.0)
+            if failed and err is None:
+                err = RuntimeError("the C4 host batch segment could not be shared on every rank")
+        if err is not None:
+            raise err
         return _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan)
     finally:
         if dist is not None:
@@ -346,6 +359,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg at N > 1")
     ap.add_argument("--c4-scans", type=int, default=65536, help="C4: scans of the one shared batch")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-timeout", type=float, default=240.0, help="seconds before the C4 leg is abandoned")
     ap.add_argument("--no-alone", action="store_true", help="skip the producer-alone timing (profiled runs)")
     args = ap.parse_args()
 
@@ -515,10 +529,32 @@ def main():
         ctx.sync()
         out["philox_scans_per_s"] = round(S * args.steps / (time.perf_counter() - t0), 1)
     if args.c4 or (world > 1 and not args.no_c4):
+        # The main line stands on its own: a C4 leg that fails is reported in it, and one that
+        # does not finish in --c4-timeout seconds (a collective that never completes on some
+        # node) ends every rank with the main line printed and the leg marked as timed out.
+        import threading
+
+        done, lock = threading.Event(), threading.Lock()
+
+        def watchdog():
+            if not done.wait(args.c4_timeout):
+                with lock:
+                    if done.is_set():
+                        return
+                    if rank == 0:
+                        line = dict(out, c4={"error": "timeout: the C4 leg did not finish in %.0f s" % args.c4_timeout})
+                        print(json.dumps(line), flush=True)
+                    sys.stderr.flush()
+                    os._exit(0)
+
+        threading.Thread(target=watchdog, daemon=True).start()
         try:
-            out["c4"] = c4_leg(args, rank, world, dist, ctx, L)
-        except Exception as e:  # the main line stands on its own; report the leg's failure in it
-            out["c4"] = {"error": "%s: %s" % (type(e).__name__, e)}
+            c4 = c4_leg(args, rank, world, dist, ctx, L)
+        except Exception as e:
+            c4 = {"error": "%s: %s" % (type(e).__name__, e)}
+        with lock:
+            done.set()
+        out["c4"] = c4
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
