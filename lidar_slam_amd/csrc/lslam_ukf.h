@@ -64,6 +64,8 @@ __device__ __forceinline__ double wrap_angle(double a) {
 __device__ __attribute__((noinline)) double ukf_sin(double x) { return sin(x); }
 __device__ __attribute__((noinline)) double ukf_cos(double x) { return cos(x); }
 __device__ __attribute__((noinline)) double ukf_atan2(double y, double x) { return atan2(y, x); }
+// sin and cos of one argument share its reduction (one call instead of two)
+__device__ __attribute__((noinline)) void ukf_sincos(double x, double *s, double *c) { sincos(x, s, c); }
 
 struct UkfConst {
     double Wm[7], Wc[7];
@@ -87,12 +89,13 @@ struct UkfLds {
     double *Y;     // [7][2L] measurement sigmas, then residuals rz_k
     double *yr;    // [2L] innovation residual_h(z, zp)
     double *wsc;   // [7][2L] Wm_k ukf_sin(phi_kj), Wm_k ukf_cos(phi_kj)
+    double *rinv;  // [2L] 1 / R_diag
     static __host__ __device__ int doubles(int L) {
-        return 21 + 21 + 98 + 28 + 7 + 16 + 14 + 21 + 7 * 2 * L + 2 * L + 7 * 2 * L;
+        return 21 + 21 + 98 + 28 + 7 + 16 + 14 + 21 + 7 * 2 * L + 2 * L + 7 * 2 * L + 2 * L;
     }
     __device__ void carve(double *base, int L) {
         sig = base; Dx = sig + 21; aug = Dx + 21; G = aug + 98; bv = G + 28; xv = bv + 7; tw = xv + 16;
-        T = tw + 14; Y = T + 21; yr = Y + 7 * 2 * L; wsc = yr + 2 * L;
+        T = tw + 14; Y = T + 21; yr = Y + 7 * 2 * L; wsc = yr + 2 * L; rinv = wsc + 7 * 2 * L;
     }
 };
 
@@ -121,8 +124,10 @@ __device__ __forceinline__ void sigma_point(int k, const double x[3], const doub
 // UKFMethods.py:17-24 transition_function (intended form)
 __device__ __forceinline__ void fx(const double s[3], double dt, double u0, double u1, double wr, double wb,
                                    double o[3]) {
-    const double c = (wr / 2.0) * ukf_cos(s[2]);
-    const double sn = (wr / 2.0) * ukf_sin(s[2]);
+    double sv, cv;
+    ukf_sincos(s[2], &sv, &cv);
+    const double c = (wr / 2.0) * cv;
+    const double sn = (wr / 2.0) * sv;
     const double k0 = (-1.0 * wr) / wb, k1 = (1.0 * wr) / wb;
     const double b0 = c * u0 + c * u1;
     const double b1 = sn * u0 + sn * u1;
@@ -166,8 +171,10 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         __syncthreads();
         if (lane < 7) {
             const double d = S.sig[3 * lane + 2] - S.sig[2];
-            S.tw[2 * lane] = ukf_sin(d) * C.Wm[lane];
-            S.tw[2 * lane + 1] = ukf_cos(d) * C.Wm[lane];
+            double sv, cv;
+            ukf_sincos(d, &sv, &cv);
+            S.tw[2 * lane] = sv * C.Wm[lane];
+            S.tw[2 * lane + 1] = cv * C.Wm[lane];
         }
         __syncthreads();
         // UKFMethods.py:37-45 state_mean (intended form), evaluated about sigma point 0 (see
@@ -242,8 +249,10 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
     for (int e = lane; e < npair; e += 64) {
         const int k = e / C.L, j = e - k * C.L;
         const double dph = S.Y[k * m2 + 2 * j + 1] - S.Y[2 * j + 1];
-        S.wsc[k * m2 + 2 * j] = ukf_sin(dph) * C.Wm[k];
-        S.wsc[k * m2 + 2 * j + 1] = ukf_cos(dph) * C.Wm[k];
+        double sv, cv;
+        ukf_sincos(dph, &sv, &cv);
+        S.wsc[k * m2 + 2 * j] = sv * C.Wm[k];
+        S.wsc[k * m2 + 2 * j + 1] = cv * C.Wm[k];
     }
     __syncthreads();
     // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals.
@@ -271,6 +280,7 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         S.yr[2 * j + 1] = wrap_angle(z[2 * j + 1] - pm);
     }
     __syncthreads();
+    for (int m = lane; m < m2; m += 64) S.rinv[m] = 1.0 / Rd[m];
     // ---- residuals rz_k on the pairs (inactive slots -> 0)
 #pragma unroll 1
     for (int e = lane; e < npair; e += 64) {
@@ -297,11 +307,19 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
             k = lane - 28;
             l = -1;
         }
-        double acc = 0.0;
+        // four partial sums over m (ILP for the dependent FMA chain), then summed in order
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         const double *yk = S.Y + k * m2;
         const double *yl = (l >= 0) ? S.Y + l * m2 : S.yr;
-#pragma unroll 1
-        for (int m = 0; m < m2; m++) acc += (yk[m] / Rd[m]) * yl[m];
+        int m = 0;
+        for (; m + 4 <= m2; m += 4) {
+            a0 = __builtin_fma(yk[m] * S.rinv[m], yl[m], a0);
+            a1 = __builtin_fma(yk[m + 1] * S.rinv[m + 1], yl[m + 1], a1);
+            a2 = __builtin_fma(yk[m + 2] * S.rinv[m + 2], yl[m + 2], a2);
+            a3 = __builtin_fma(yk[m + 3] * S.rinv[m + 3], yl[m + 3], a3);
+        }
+        for (; m < m2; m++) a0 = __builtin_fma(yk[m] * S.rinv[m], yl[m], a0);
+        const double acc = (a0 + a1) + (a2 + a3);
         if (lane < 28) S.G[lane] = acc;
         else S.bv[lane - 28] = acc;
     }
