@@ -64,8 +64,13 @@ __device__ __forceinline__ double wrap_angle(double a) {
 __device__ __attribute__((noinline)) double ukf_sin(double x) { return sin(x); }
 __device__ __attribute__((noinline)) double ukf_cos(double x) { return cos(x); }
 __device__ __attribute__((noinline)) double ukf_atan2(double y, double x) { return atan2(y, x); }
-// sin and cos of one argument share its reduction (one call instead of two)
-__device__ __attribute__((noinline)) void ukf_sincos(double x, double *s, double *c) { sincos(x, s, c); }
+// sin and cos of one argument share its reduction (one call instead of two); returned by
+// value (.x = sin, .y = cos) so the results come back in registers, not through scratch
+__device__ __attribute__((noinline)) double2 ukf_sincos(double x) {
+    double s, c;
+    sincos(x, &s, &c);
+    return make_double2(s, c);
+}
 
 struct UkfConst {
     double Wm[7], Wc[7];
@@ -124,10 +129,9 @@ __device__ __forceinline__ void sigma_point(int k, const double x[3], const doub
 // UKFMethods.py:17-24 transition_function (intended form)
 __device__ __forceinline__ void fx(const double s[3], double dt, double u0, double u1, double wr, double wb,
                                    double o[3]) {
-    double sv, cv;
-    ukf_sincos(s[2], &sv, &cv);
-    const double c = (wr / 2.0) * cv;
-    const double sn = (wr / 2.0) * sv;
+    const double2 scv = ukf_sincos(s[2]);
+    const double c = (wr / 2.0) * scv.y;
+    const double sn = (wr / 2.0) * scv.x;
     const double k0 = (-1.0 * wr) / wb, k1 = (1.0 * wr) / wb;
     const double b0 = c * u0 + c * u1;
     const double b1 = sn * u0 + sn * u1;
@@ -171,10 +175,9 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
         __syncthreads();
         if (lane < 7) {
             const double d = S.sig[3 * lane + 2] - S.sig[2];
-            double sv, cv;
-            ukf_sincos(d, &sv, &cv);
-            S.tw[2 * lane] = sv * C.Wm[lane];
-            S.tw[2 * lane + 1] = cv * C.Wm[lane];
+            const double2 scv = ukf_sincos(d);
+            S.tw[2 * lane] = scv.x * C.Wm[lane];
+            S.tw[2 * lane + 1] = scv.y * C.Wm[lane];
         }
         __syncthreads();
         // UKFMethods.py:37-45 state_mean (intended form), evaluated about sigma point 0 (see
@@ -249,10 +252,9 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
     for (int e = lane; e < npair; e += 64) {
         const int k = e / C.L, j = e - k * C.L;
         const double dph = S.Y[k * m2 + 2 * j + 1] - S.Y[2 * j + 1];
-        double sv, cv;
-        ukf_sincos(dph, &sv, &cv);
-        S.wsc[k * m2 + 2 * j] = sv * C.Wm[k];
-        S.wsc[k * m2 + 2 * j + 1] = cv * C.Wm[k];
+        const double2 scv = ukf_sincos(dph);
+        S.wsc[k * m2 + 2 * j] = scv.x * C.Wm[k];
+        S.wsc[k * m2 + 2 * j + 1] = scv.y * C.Wm[k];
     }
     __syncthreads();
     // ---- z_mean per landmark (lanes), innovation; means kept in yr until the residuals.
