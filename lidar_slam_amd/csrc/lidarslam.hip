@@ -1317,6 +1317,80 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
     }
 }
 
+// The same without LDS: one wave per (chunk, draw), lanes = 64 consecutive
+// steps i of the draw, so each load is one coalesced 128-byte (u16) read
+// straight from HBM and a wave keeps RW windows of loads in flight.  The
+// trackers c0, c1 are wave-uniform: a window's matches j_i == c come out of one
+// compare as a lane mask; the lowest matching lane l moves c to i0 + l, after
+// which only lanes above l can match the new c (j_i <= i) - a hop is rare
+// (probability 1/(i+1) per step).  Per window: one load, the mask, two compares.
+constexpr int RW = 8;  // windows of 64 steps in flight per wave
+template <typename JT>
+__global__ __launch_bounds__(64) void resolve_walk_kernel(const KArgs a) {
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
+    const int64_t total = (int64_t)B.n_chunks * D;
+    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
+        const int c = (int)(e / D);
+        const uint32_t d = (uint32_t)(e - (int64_t)c * D);
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        const uint32_t K = (uint32_t)N - 1u;
+        const JT *Jd = (const JT *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)d * K;  // step i at K - i
+        uint32_t c0 = 0, c1 = 1;
+        auto track = [&](uint32_t jv, uint32_t i0) {
+            uint64_t m0 = ballot(jv == c0), m1 = ballot(jv == c1);
+            while (m0) {
+                const int l = ffs64(m0);
+                c0 = i0 + (uint32_t)l;
+                m0 = ballot(jv == c0) & ((~0ull << l) << 1);
+            }
+            while (m1) {
+                const int l = ffs64(m1);
+                c1 = i0 + (uint32_t)l;
+                m1 = ballot(jv == c1) & ((~0ull << l) << 1);
+            }
+        };
+        // RW windows at a time, their loads issued together; in the last group the lanes past K
+        // read step K (in range) and never match
+        for (uint32_t ib = 2; ib <= K; ib += 64u * RW) {
+            uint32_t raw[RW];
+            if (ib + 64u * RW - 1u <= K) {
+                const JT *q = Jd + (K - ib - (uint32_t)lane);
+#pragma unroll
+                for (int u = 0; u < RW; u++) raw[u] = (uint32_t)q[-64 * u];
+#pragma unroll
+                for (int u = 0; u < RW; u++) {
+                    const uint32_t i = ib + 64u * (uint32_t)u + (uint32_t)lane;
+                    track(raw[u] & step_mask(i), ib + 64u * (uint32_t)u);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < RW; u++) {
+                    const uint32_t i = ib + 64u * (uint32_t)u + (uint32_t)lane;
+                    raw[u] = (uint32_t)Jd[K - (i <= K ? i : K)];
+                }
+#pragma unroll
+                for (int u = 0; u < RW; u++) {
+                    const uint32_t i0 = ib + 64u * (uint32_t)u, i = i0 + (uint32_t)lane;
+                    if (i0 > K) break;
+                    track(i <= K ? (raw[u] & step_mask(i)) : 0xffffffffu, i0);
+                }
+            }
+        }
+        if (lane == 0) {
+            const uint32_t j1 = (uint32_t)Jd[K - 1u] & 1u;
+            int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)a.ep_d0;
+            draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
+            draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------
 // chunk_kernel: one wave per chunk, A4-A8 with the draws given
 // ------------------------------------------------------------------------
@@ -1879,6 +1953,7 @@ struct lslam_ctx {
     size_t cscr_bytes;
     // grid cap of the one-wave consumer kernels (resolve, chunk, fix-up, post)
     int consumer_wgs;
+    int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
     int rng_ppw;
@@ -2001,6 +2076,10 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->cscr = nullptr;
     c->cscr_bytes = 0;
     c->consumer_wgs = 1 << 30;
+    {
+        const char *e = getenv("LSLAM_RESOLVE_TILED");
+        c->resolve_walk = (e && atoi(e) != 0) ? 0 : 1;
+    }
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
     if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
@@ -2542,7 +2621,9 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
     int off = 0;
     k.off_blk = off; off += align16(4 * (2 * 624 + 64));  // two block slots + the head pad
     k.off_fl = off; off += align16(4 * F_NFLAGS);
-    k.off_tbl = off; off += (N - 1 <= (int)RT_KMAX) ? align16(4 * RT_DWORDS) : 0;
+    // the reject table: table mode is chosen per chunk (N - 1 <= RT_KMAX), so a batch whose
+    // largest chunk is bigger may still parse its small chunks with it
+    k.off_tbl = off; off += k.rt_all ? align16(4 * RT_DWORDS) : 0;
     k.rng_pipe_bytes = off;
     lds = off * ppw;
     return LSLAM_OK;
@@ -2640,6 +2721,14 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     const int64_t need = ((int64_t)De * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
     const int lds = need <= 16 * 1024 ? (int)need : 0;
     k.res_g = lds;  // staging capacity in bytes
+    if (lds == 0 && c->resolve_walk) {  // steps streamed from HBM, waves over (chunk, draw)
+        const int64_t items = (int64_t)k.b.n_chunks * De;
+        const dim3 grid(launch_cap(c, items > (1 << 20) ? (1 << 20) : items)), block(64);
+        if (k.j8) hipLaunchKernelGGL(resolve_walk_kernel<uint8_t>, grid, block, 0, c->stream, k);
+        else hipLaunchKernelGGL(resolve_walk_kernel<uint16_t>, grid, block, 0, c->stream, k);
+        HIPCHK(hipGetLastError());
+        return LSLAM_OK;
+    }
     if (lds == 0) {  // steps streamed through LDS tiles, waves over (chunk, 64 draws)
         const int ngroups = (De + 63) / 64;
         const int64_t items = (int64_t)k.b.n_chunks * ngroups;

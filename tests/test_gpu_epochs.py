@@ -159,3 +159,28 @@ def test_epochs_with_an_early_stop(ctx):
     mo, md, _ = orc.ransac(xys[2], 20.0, trials, state=st)
     assert np.array_equal(b["mask"][2 * n:3 * n], mo)
     assert np.array_equal(b["mt_state"][2, :624], st.key) and b["mt_state"][2, 624] == st.pos.value
+
+
+@pytest.mark.parametrize("top", [200, 300])
+def test_walk_resolve_ragged_chunks(ctx, top):
+    """Unstaged resolves (a chunk's steps over the 16 KiB stage): one wave per (chunk, draw),
+    lanes = steps.  Chunks of 3..top points in one batch (K from 2, a single partial window with
+    many tracker hops, to several 512-step groups), u8 (top 200) and u16 (top 300) steps: every
+    draw and the end states equal the oracle's choice(N, 2) sequence.  Table-mode (N <= 128) and
+    mask-mode chunks share the scans, both orders (the producer's reject table must exist whenever
+    any chunk can use it, not only when the largest chunk does)."""
+    from lidar_slam_amd import pipeline as pl
+    sizes = [top, 3, 4, 5, 30, 64, 65, 66, 129, top]
+    S = 3
+    sco = (np.arange(S + 1) * len(sizes)).astype(np.int32)
+    cpo = np.concatenate([[0], np.cumsum(sizes * S)]).astype(np.int32)
+    trials = 120  # 121 draws x (top - 1) steps > 16 KiB
+    seeds = np.arange(S, dtype=np.uint32) + 7100
+    draws, state = pl.hyp_mt19937(ctx, sco, cpo, seeds=seeds, max_trials=trials)
+    for s in range(S):
+        st = orc.MTState(seed=int(seeds[s]))
+        for c in range(sco[s], sco[s + 1]):
+            nc = int(cpo[c + 1] - cpo[c])
+            ref = np.array([st.choice2(nc) for _ in range(trials + 1)])
+            assert np.array_equal(draws[c], ref), (top, s, c, nc)
+        assert np.array_equal(state[s, :624], st.key) and state[s, 624] == st.pos.value
