@@ -1324,8 +1324,7 @@ __global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngro
 // compare as a lane mask; the lowest matching lane l moves c to i0 + l, after
 // which only lanes above l can match the new c (j_i <= i) - a hop is rare
 // (probability 1/(i+1) per step).  Per window: one load, the mask, two compares.
-constexpr int RW = 8;  // windows of 64 steps in flight per wave
-template <typename JT>
+template <typename JT, int RW>  // RW: windows of 64 steps in flight per wave
 __global__ __launch_bounds__(64) void resolve_walk_kernel(const KArgs a) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
@@ -1954,6 +1953,8 @@ struct lslam_ctx {
     // grid cap of the one-wave consumer kernels (resolve, chunk, fix-up, post)
     int consumer_wgs;
     int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
+    int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
+    int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
     int rng_ppw;
@@ -2068,6 +2069,9 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     lslam_ctx *c = new (std::nothrow) lslam_ctx();
     if (!c) return LSLAM_ERR_NOMEM;
     c->device = device;
+    c->n_cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&c->n_cus, hipDeviceAttributeMultiprocessorCount, device));
+    if (c->n_cus < 1) c->n_cus = 1;
     c->timing = false;
     c->scr = nullptr;
     c->scr_bytes = 0;
@@ -2079,6 +2083,10 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     {
         const char *e = getenv("LSLAM_RESOLVE_TILED");
         c->resolve_walk = (e && atoi(e) != 0) ? 0 : 1;
+    }
+    {
+        const char *e = getenv("LSLAM_EPOCH_SERIAL");
+        c->epoch_serial = (e && atoi(e) != 0) ? 1 : 0;
     }
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
@@ -2723,9 +2731,12 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
     k.res_g = lds;  // staging capacity in bytes
     if (lds == 0 && c->resolve_walk) {  // steps streamed from HBM, waves over (chunk, draw)
         const int64_t items = (int64_t)k.b.n_chunks * De;
-        const dim3 grid(launch_cap(c, items > (1 << 20) ? (1 << 20) : items)), block(64);
-        if (k.j8) hipLaunchKernelGGL(resolve_walk_kernel<uint8_t>, grid, block, 0, c->stream, k);
-        else hipLaunchKernelGGL(resolve_walk_kernel<uint16_t>, grid, block, 0, c->stream, k);
+        // beside the next epoch's producer (produce_draws): two waves per SIMD, so its parsers
+        // keep their residency (three per SIMD displaced them: C5 107 vs 78 ms per call)
+        const int64_t cap = (k.ep_count > 1 && !c->epoch_serial) ? 8 * (int64_t)c->n_cus : (1 << 20);
+        const dim3 grid(launch_cap(c, items > cap ? cap : items)), block(64);
+        if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, c->stream, k);
+        else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, c->stream, k);
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
@@ -2786,9 +2797,11 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
 // k.state_scr is the end state's area and last_slot the slot the caller releases.
 static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint32_t *final_out, int &last_slot) {
     const int D = k.T + 1;
-    // Epochs run on the ctx stream one after the other: an epoch's resolve beside the next
-    // epoch's producer slowed the parsers more than it hid (C5: 129 vs 112 ms per call)
-    if (k.ep_count > 1 && ps != c->stream) {
+    // An epoch's resolve (the lane walk on a grid of two waves per SIMD) runs on the ctx
+    // stream beside the next epoch's producer on ps, the slots alternating (C5: 78 vs 89 ms
+    // per call serial).  The LDS-tiled resolve slowed the parsers more than it hid (129 vs
+    // 112 ms): with it, or LSLAM_EPOCH_SERIAL=1, the epochs run one after the other.
+    if (k.ep_count > 1 && ps != c->stream && (c->epoch_serial || !c->resolve_walk)) {
         HIPCHK(hipEventRecord(c->ev_produced, ps));
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
         ps = c->stream;
