@@ -1,0 +1,13 @@
+# Everything profiles/<tag>_* holds, in one GPU call; each step time-limited, stop at the first failure.
+# Usage: tools/round_profile.sh <tag>   (then: python tools/profile_summary.py <tag>)
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+TAG=${1:?tag}
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+tail -1 gpurun_out/bench.log
+bash tools/profile_session.sh $TAG || exit 1
+timeout -k 10 300 python -u tools/c5bench.py --scans 4096 --reps 2 > gpurun_out/c5.json 2> gpurun_out/c5.err || { tail -20 gpurun_out/c5.err; exit 1; }
+cat gpurun_out/c5.json
+timeout -k 10 300 python -u tools/mapbench.py > gpurun_out/mapbench.json 2> gpurun_out/mapbench.err || { tail -20 gpurun_out/mapbench.err; exit 1; }
+cat gpurun_out/mapbench.json
