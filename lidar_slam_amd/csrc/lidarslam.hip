@@ -1085,6 +1085,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void sc
     }
 }
 
+// UKF step of the fused pipeline on groups of Pg lanes per scan (lslam_ukf.h: ukf_step_group),
+// after the association pass; the landmark slots [0, nchunks) take the scan's fitted chunk
+// origins (LMK_FROM_RANSAC) exactly as the post pass's corg does (models with LSLAM_VALID)
+__global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg) {
+    const lslam_scan_batch &B = a.b;
+    const int lane = (int)threadIdx.x;
+    const int g = lane & (Pg - 1);
+    const int s = (int)blockIdx.x * (64 / Pg) + lane / Pg;
+    if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);  // the post pass's level
+    if (s >= B.n_scans) return;  // whole groups only: the butterfly stays inside a group
+    double x[3], Pm[9];
+    for (int i = 0; i < 3; i++) x[i] = B.ukf_x[3 * (size_t)s + i];
+    for (int i = 0; i < 9; i++) Pm[i] = B.ukf_P[9 * (size_t)s + i];
+    const double u0 = B.ukf_u[2 * (size_t)s], u1 = B.ukf_u[2 * (size_t)s + 1];
+    const int Lu = a.ukf.L;
+    const double *lm = B.ukf_lmk + (size_t)s * 2 * Lu;
+    const int c0 = B.scan_chunk_off[s];
+    const int nfuse = (a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC) ? B.scan_chunk_off[s + 1] - c0 : 0;
+    auto lmk_fn = [&](int j, double &px, double &py) {
+        px = lm[2 * j];
+        py = lm[2 * j + 1];
+        if (j < nfuse) {
+            const lslam_chunk_model &m = B.models[c0 + j];
+            if (m.flags & LSLAM_VALID) {
+                px = m.ox;
+                py = m.oy;
+            }
+        }
+        return true;
+    };
+    ukf_step_group(x, Pm, u0, u1, B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, a.ukf.flags, g, Pg);
+    if (g == 0) {
+        for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = x[i];
+        for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
+    }
+}
+
 // ------------------------------------------------------------------------
 // rng_kernel: the chained parity stream of one scan -> every chunk's draws
 // (wave 0 parses, wave 1 twists ahead and resolves; lslam_rng_pipe.h)
@@ -1954,6 +1991,7 @@ struct lslam_ctx {
     int consumer_wgs;
     int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
     int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
+    int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
     int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
@@ -2087,6 +2125,10 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     {
         const char *e = getenv("LSLAM_EPOCH_SERIAL");
         c->epoch_serial = (e && atoi(e) != 0) ? 1 : 0;
+    }
+    {
+        const char *e = getenv("LSLAM_UKF_LANES");
+        c->ukf_lanes = (e && atoi(e) == 0) ? 0 : 1;
     }
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
@@ -3063,10 +3105,21 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     // slows the resolve -> consensus chain more than it saves, 1.23 -> 1.27-1.32 ms on C3)
     const bool ukf_side = p->hyp_source != LSLAM_HYP_MT19937 && u &&
                           !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
-    const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u && !ukf_side ? MODE_UKF : 0);
-    if (assoc || (u && !ukf_side)) {
-        st = build_args(kp, b, p, ukf_side ? nullptr : u, pmode, lds_post);
+    // the UKF of the fused call on lane groups after the association pass (not in MAP mode,
+    // whose measurements come out of the association walk itself)
+    const bool ukf_lane = u && !ukf_side && !(u->flags & LSLAM_UKF_MAP) && c->ukf_lanes;
+    const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u && !ukf_side && !ukf_lane ? MODE_UKF : 0);
+    if (assoc || (u && !ukf_side && !ukf_lane)) {
+        st = build_args(kp, b, p, (ukf_side || ukf_lane) ? nullptr : u, pmode, lds_post);
         if (st) return st;
+    }
+    KArgs kl;
+    if (ukf_lane) {
+        int lds_l = 0;
+        st = build_args(kl, b, p, u, MODE_UKF, lds_l);
+        if (st) return st;
+        if ((u->flags & LSLAM_UKF_LMK_FROM_RANSAC) && !b->models)
+            return set_err(LSLAM_ERR_ARG, "LSLAM_UKF_LMK_FROM_RANSAC needs the chunk models");
     }
     KArgs ku;
     int lds_u = 0;
@@ -3130,6 +3183,14 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
+    if (ukf_lane) {
+        int Pg = 1;  // lanes per scan: the landmarks, up to a wave
+        while (Pg < u->n_landmarks && Pg < 64) Pg <<= 1;
+        const int per = 64 / Pg;
+        hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((b->n_scans + per - 1) / per)), dim3(64), 0, c->stream, kl,
+                           Pg);
+        HIPCHK(hipGetLastError());
+    }
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
     if ((st = end_call(c))) return st;

@@ -423,4 +423,211 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
     return ok;
 }
 
+// The same step for one scan on a GROUP of Pg lanes (Pg a power of two <= 64; 64 / Pg scans
+// per wave): registers only, no LDS and no barriers.  Every lane of the group runs the predict,
+// the sigma points and the final solve redundantly (identical inputs give identical results);
+// the measurement work is split by landmark (lane g takes j = g, g + Pg, ...), each lane
+// accumulates its landmarks' share of G = Y R^-1 Y^T and b = Y R^-1 y, and an xor butterfly over
+// the group sums them (commutative pairs: every lane ends with the same G and b).  The sums keep
+// the sigma order k = 0..6; M X = [b | Dx] is solved directly (Gauss-Jordan, partial pivoting)
+// instead of forming M^-1, so the last bits differ from ukf_step; both are held to the 50-digit
+// evaluation per component (tests/test_gpu_ukf_exact.py).
+template <typename LmkFn>
+__device__ bool ukf_step_group(double x[3], double P[9], double u0, double u1, const double *z, const double *Rd,
+                               LmkFn lmk, const UkfConst &C, int flags, int g, int Pg) {
+    bool ok = true;
+    double U[9];
+    double sig[21];
+    if (flags & 1) {  // ---- predict
+        {
+            double A[9];
+#pragma unroll
+            for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
+            chol3_upper(A, U);
+        }
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            double sg[3];
+            sigma_point(k, x, U, sg);
+            fx(sg, C.dt, u0, u1, C.wr, C.wb, sig + 3 * k);
+        }
+        double s0 = 0.0, s1 = 0.0, ss = 0.0, sc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double2 scv = ukf_sincos(sig[3 * k + 2] - sig[2]);
+            s0 += (sig[3 * k] - sig[0]) * C.Wm[k];
+            s1 += (sig[3 * k + 1] - sig[1]) * C.Wm[k];
+            ss += scv.x * C.Wm[k];
+            sc += scv.y * C.Wm[k];
+        }
+        const double xm0 = sig[0] + s0, xm1 = sig[1] + s1;
+        const double xm2 = wrap_angle(sig[2] + ukf_atan2(ss, sc));
+        double Pn[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) Pn[i] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double y[3] = {sig[3 * k] - xm0, sig[3 * k + 1] - xm1, wrap_angle(sig[3 * k + 2] - xm2)};
+            const double w = C.Wc[k];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) Pn[3 * i + j] = Pn[3 * i + j] + w * (y[i] * y[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) P[i] = Pn[i] + C.Q[i];
+        x[0] = xm0;
+        x[1] = xm1;
+        x[2] = xm2;
+    }
+    if (!(flags & 2)) return ok;
+    {
+        double A[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
+        chol3_upper(A, U);
+        if (!(U[0] > 0.0) || !(U[4] > 0.0) || !(U[8] > 0.0)) ok = false;
+    }
+    double Dx[21];
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        sigma_point(k, x, U, sig + 3 * k);
+        Dx[3 * k] = sig[3 * k] - x[0];
+        Dx[3 * k + 1] = sig[3 * k + 1] - x[1];
+        Dx[3 * k + 2] = wrap_angle(sig[3 * k + 2] - x[2]);
+    }
+    // G = Y R^-1 Y^T (upper triangle, row-major k <= l) and b = Y R^-1 y over the landmarks
+    double G[28], bv[7];
+#pragma unroll
+    for (int e = 0; e < 28; e++) G[e] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) bv[k] = 0.0;
+#pragma unroll 1
+    for (int j = g; j < C.L; j += Pg) {
+        double px, py;
+        if (!lmk(j, px, py)) continue;  // an inactive slot adds exactly nothing
+        double d[7], ph[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double dx = px - sig[3 * k], dy = py - sig[3 * k + 1];
+            d[k] = cr_sqrt(dx * dx + dy * dy);
+            ph[k] = wrap_angle(ukf_atan2(dy, dx) - sig[3 * k + 2]);
+        }
+        // z_mean about sigma 0 (as in ukf_step)
+        double dm = 0.0, ss = 0.0, sc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double2 scv = ukf_sincos(ph[k] - ph[0]);
+            dm += (d[k] - d[0]) * C.Wm[k];
+            ss += scv.x * C.Wm[k];
+            sc += scv.y * C.Wm[k];
+        }
+        dm = d[0] + dm;
+        const double pm = wrap_angle(ph[0] + ukf_atan2(ss, sc));
+        const double yr0 = z[2 * j] - dm, yr1 = wrap_angle(z[2 * j + 1] - pm);
+        const double ri0 = 1.0 / Rd[2 * j], ri1 = 1.0 / Rd[2 * j + 1];
+        double r0[7], r1[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            r0[k] = d[k] - dm;
+            r1[k] = wrap_angle(ph[k] - pm);
+        }
+        int e = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double w0 = r0[k] * ri0, w1 = r1[k] * ri1;
+#pragma unroll
+            for (int l = k; l < 7; l++, e++) {
+                G[e] = __builtin_fma(w0, r0[l], G[e]);
+                G[e] = __builtin_fma(w1, r1[l], G[e]);
+            }
+            bv[k] = __builtin_fma(w0, yr0, bv[k]);
+            bv[k] = __builtin_fma(w1, yr1, bv[k]);
+        }
+    }
+    // the group's sum of G and b
+#pragma unroll 1
+    for (int o = 1; o < Pg; o <<= 1) {
+#pragma unroll
+        for (int e = 0; e < 28; e++) G[e] += __shfl_xor(G[e], o);
+#pragma unroll
+        for (int k = 0; k < 7; k++) bv[k] += __shfl_xor(bv[k], o);
+    }
+    // [M | b | Dx], M = W^-1 + G; Gauss-Jordan with partial pivoting (first largest |pivot|)
+    double A[7][11];
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+#pragma unroll
+        for (int cc = 0; cc < 7; cc++) {
+            const int k = r < cc ? r : cc, l = r < cc ? cc : r;
+            double v = G[k * 7 - (k * (k - 1)) / 2 + (l - k)];
+            if (r == cc) v += 1.0 / C.Wc[r];
+            A[r][cc] = v;
+        }
+        A[r][7] = bv[r];
+#pragma unroll
+        for (int j = 0; j < 3; j++) A[r][8 + j] = Dx[3 * r + j];
+    }
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+        int piv = c;
+        double best = fabs(A[c][c]);
+#pragma unroll
+        for (int r = c + 1; r < 7; r++) {
+            const double v = fabs(A[r][c]);
+            if (v > best) {
+                best = v;
+                piv = r;
+            }
+        }
+        if (!(best > 0.0)) ok = false;
+#pragma unroll
+        for (int r = c + 1; r < 7; r++) {
+            if (piv == r) {
+#pragma unroll
+                for (int cc = 0; cc < 11; cc++) {
+                    const double t = A[c][cc];
+                    A[c][cc] = A[r][cc];
+                    A[r][cc] = t;
+                }
+            }
+        }
+        const double dpiv = A[c][c];
+#pragma unroll
+        for (int cc = 0; cc < 11; cc++) A[c][cc] = A[c][cc] / dpiv;
+#pragma unroll
+        for (int r = 0; r < 7; r++) {
+            if (r == c) continue;
+            const double f = A[r][c];
+            if (f != 0.0) {
+#pragma unroll
+                for (int cc = 0; cc < 11; cc++) A[r][cc] = A[r][cc] - f * A[c][cc];
+            }
+        }
+    }
+    // x += Dx^T M^-1 b ;  P -= Dx^T (W Dx - M^-1 Dx)
+    double dxn[3], KSK[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) sacc += Dx[3 * k + i] * A[k][7];
+        dxn[i] = sacc;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double sacc = 0.0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) sacc += Dx[3 * k + i] * (C.Wc[k] * Dx[3 * k + j] - A[k][8 + j]);
+            KSK[3 * i + j] = sacc;
+        }
+#pragma unroll
+    for (int i = 0; i < 3; i++) x[i] = x[i] + dxn[i];
+#pragma unroll
+    for (int i = 0; i < 9; i++) P[i] = P[i] - KSK[i];
+    return ok;
+}
+
 }  // namespace lslam
