@@ -1280,6 +1280,60 @@ __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     }
 }
 
+// The staged walk without LDS (u8 steps, C3): lanes = draws, each lane loads its own row 16
+// steps at a time (one unaligned 16-byte load; the 64 rows of a group lie in ~50 cache lines
+// that stay in the vector L1) and walks the bytes from registers.  Beside the producer, whose
+// workgroups hold most of each CU's LDS, the staged resolve fits only ~2 waves per CU.
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+__global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
+    for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        const uint32_t K = (uint32_t)N - 1u;
+        const uint8_t *J = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0;
+        int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)a.ep_d0;
+        for (uint32_t d0 = 0; d0 < D; d0 += 64) {
+            const uint32_t d = d0 + (uint32_t)lane;
+            const bool live = d < D;
+            const uint8_t *row = J + (size_t)(live ? d : d0) * K;  // step i at row[K - i]
+            uint32_t c0 = 0, c1 = 1;
+            uint32_t i0 = 2;
+            // 16 steps i0 .. i0 + 15 = bytes K - i0 - 15 .. K - i0, walked from the top byte down
+            for (; i0 + 15u <= K; i0 += 16u) {
+                const uint4 v = load16_unaligned(row + (K - i0 - 15u));
+                const uint32_t w[4] = {v.w, v.z, v.y, v.x};
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint32_t i = i0 + (uint32_t)u;
+                    const uint32_t j = ((w[u >> 2] >> (8 * (3 - (u & 3)))) & 0xffu) & step_mask(i);
+                    c0 = (j == c0) ? i : c0;
+                    c1 = (j == c1) ? i : c1;
+                }
+            }
+            for (; i0 <= K; i0++) {
+                const uint32_t j = (uint32_t)row[K - i0] & step_mask(i0);
+                c0 = (j == c0) ? i0 : c0;
+                c1 = (j == c1) ? i0 : c1;
+            }
+            if (live) {
+                const uint32_t j1 = (uint32_t)row[K - 1u] & 1u;
+                draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
+                draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
+            }
+        }
+    }
+}
+
 // Chunks whose steps do not fit the 16 KiB stage (C5: 2049 draws x 4095 steps
 // x 2 B = 16.8 MB per chunk).  One wave per (chunk, group of 64 draws), lanes =
 // draws as in resolve_draws_fwd, but the steps stream through an LDS tile of
@@ -1992,6 +2046,7 @@ struct lslam_ctx {
     int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
     int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
     int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
+    int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage)
     int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
@@ -2129,6 +2184,10 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     {
         const char *e = getenv("LSLAM_UKF_LANES");
         c->ukf_lanes = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    {
+        const char *e = getenv("LSLAM_RESOLVE_REG");
+        c->resolve_reg = (e && atoi(e) == 0) ? 0 : 1;
     }
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
@@ -2789,6 +2848,12 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         const int tl = 64 * (RB + 4) * esz;
         if (k.j8) hipLaunchKernelGGL(resolve_big_kernel<uint8_t>, grid, block, tl, c->stream, k, ngroups);
         else hipLaunchKernelGGL(resolve_big_kernel<uint16_t>, grid, block, tl, c->stream, k, ngroups);
+        HIPCHK(hipGetLastError());
+        return LSLAM_OK;
+    }
+    if (k.j8 && c->resolve_reg) {  // no LDS: the producer's workgroups hold most of it
+        const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
+        hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, c->stream, k);
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
