@@ -3249,8 +3249,10 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     }
     if (st) return st;
     if (ukf_lane) {
-        int Pg = 1;  // lanes per scan: the landmarks, up to a wave
-        while (Pg < u->n_landmarks && Pg < 64) Pg <<= 1;
+        // lanes per scan: about two landmarks per lane, up to a wave (C3: 16 lanes, 4 scans per
+        // wave, one round of waves beside the producer; one landmark per lane: +1 %, five: +2 %)
+        int Pg = 1;
+        while (Pg < (u->n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
         const int per = 64 / Pg;
         hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((b->n_scans + per - 1) / per)), dim3(64), 0, c->stream, kl,
                            Pg);
