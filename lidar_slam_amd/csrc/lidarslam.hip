@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void sc
 // UKF step of the fused pipeline on groups of Pg lanes per scan (lslam_ukf.h: ukf_step_group),
 // after the association pass; the landmark slots [0, nchunks) take the scan's fitted chunk
 // origins (LMK_FROM_RANSAC) exactly as the post pass's corg does (models with LSLAM_VALID)
-__global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg) {
+__global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg, int fuse) {
     const lslam_scan_batch &B = a.b;
     const int lane = (int)threadIdx.x;
     const int g = lane & (Pg - 1);
@@ -1102,7 +1102,8 @@ __global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg) {
     const int Lu = a.ukf.L;
     const double *lm = B.ukf_lmk + (size_t)s * 2 * Lu;
     const int c0 = B.scan_chunk_off[s];
-    const int nfuse = (a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC) ? B.scan_chunk_off[s + 1] - c0 : 0;
+    // fuse: a pipeline call's post pass, whose chunk models exist (the stand-alone step has none)
+    const int nfuse = (fuse && (a.ukf.flags & LSLAM_UKF_LMK_FROM_RANSAC)) ? B.scan_chunk_off[s + 1] - c0 : 0;
     auto lmk_fn = [&](int j, double &px, double &py) {
         px = lm[2 * j];
         py = lm[2 * j + 1];
@@ -1120,6 +1121,16 @@ __global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg) {
         for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = x[i];
         for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
     }
+}
+
+// lanes per scan: about two landmarks per lane, up to a wave (C3: 16 lanes, 4 scans per wave,
+// one round of waves beside the producer; one landmark per lane: +1 % per C3 step, five: +2 %)
+static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream, bool fuse) {
+    int Pg = 1;
+    while (Pg < (n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
+    const int per = 64 / Pg;
+    hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((k.b.n_scans + per - 1) / per)), dim3(64), 0, stream, k, Pg,
+                       fuse ? 1 : 0);
 }
 
 // ------------------------------------------------------------------------
@@ -2689,7 +2700,10 @@ static int run_scan_kernel(lslam_ctx *c, const KArgs &k, int lds, int timer) {
     });
     int st = timer_begin(c, timer);
     if (st) return st;
-    if (MODE == MODE_ASSOC || MODE == MODE_UKF) {  // stand-alone association / UKF: no producer beside them
+    if (MODE == MODE_UKF && c->ukf_lanes && !(k.ukf.flags & LSLAM_UKF_MAP)) {  // stand-alone UKF: lane groups
+        launch_ukf_group(k, k.ukf.L, c->stream, false);
+        HIPCHK(hipGetLastError());
+    } else if (MODE == MODE_ASSOC || MODE == MODE_UKF) {  // stand-alone association / UKF: no producer beside them
         hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), dim3((unsigned)k.b.n_scans), dim3(64), lds,
                            c->stream, k);
         HIPCHK(hipGetLastError());
@@ -3198,10 +3212,14 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         // after the previous call (its outputs may be this step's inputs) and the latest copies
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_call, 0));
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_copy, 0));
-        static std::once_flag once;
-        std::call_once(once, [] { set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>); });
-        hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_u,
-                           c->ustream, ku);
+        if (c->ukf_lanes) {
+            launch_ukf_group(ku, u->n_landmarks, c->ustream, false);
+        } else {
+            static std::once_flag once;
+            std::call_once(once, [] { set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>); });
+            hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>), dim3(launch_cap(c, b->n_scans)), dim3(64),
+                               lds_u, c->ustream, ku);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev_ukf, c->ustream));
     }
@@ -3249,13 +3267,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     }
     if (st) return st;
     if (ukf_lane) {
-        // lanes per scan: about two landmarks per lane, up to a wave (C3: 16 lanes, 4 scans per
-        // wave, one round of waves beside the producer; one landmark per lane: +1 %, five: +2 %)
-        int Pg = 1;
-        while (Pg < (u->n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
-        const int per = 64 / Pg;
-        hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((b->n_scans + per - 1) / per)), dim3(64), 0, c->stream, kl,
-                           Pg);
+        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
         HIPCHK(hipGetLastError());
     }
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
