@@ -2058,6 +2058,7 @@ struct lslam_ctx {
     int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
     int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
     int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage)
+    int resolve_beside;  // this call's resolves will likely run beside the next call's producer
     int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // parser waves per producer workgroup (one helper each)
@@ -2200,6 +2201,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
         const char *e = getenv("LSLAM_RESOLVE_REG");
         c->resolve_reg = (e && atoi(e) == 0) ? 0 : 1;
     }
+    c->resolve_beside = 0;
     c->timing_mask = 0xffffffffu;
     c->rng_ppw = 4;
     if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
@@ -2865,7 +2867,7 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
-    if (k.j8 && c->resolve_reg) {  // no LDS: the producer's workgroups hold most of it
+    if (k.j8 && c->resolve_reg && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
         const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
         hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, c->stream, k);
         HIPCHK(hipGetLastError());
@@ -3240,6 +3242,11 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
             c->out_unknown = 0;
         }
         if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
+        // a producer that waited on the previous call (a chained stream: LandmarkMap steps) will
+        // most likely wait on this one too, so this call's resolve runs alone: the LDS-staged
+        // form is faster there (map mode 1.48 vs 1.39 ms per step); otherwise the next call's
+        // producer runs beside it and holds the LDS (C3 0.93 vs 1.03 ms)
+        c->resolve_beside = hz == 0;
         st = produce_draws(c, k, slot, c->pstream, nullptr, slot);  // slot <- the last epoch's
         if (st) return st;
     }
@@ -3353,6 +3360,7 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_slot_free[slot], 0));
     int last = slot;
     // on the main stream; the end state goes straight to mt_state_out
+    c->resolve_beside = 0;  // alone on the ctx stream
     st = produce_draws(c, k, slot, c->stream, b->mt_state_out, last);
     if (st) return st;
     HIPCHK(hipEventRecord(c->ev_slot_free[last], c->stream));
