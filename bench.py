@@ -339,8 +339,10 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 50 steps of ~1 ms: the two-stream pipeline's fill and drain (the first producer has no
+    # consumers beside it, the last consumers no producer) amortised to ~1 % of the step
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU")
     ap.add_argument("--beams", type=int, default=720)
     ap.add_argument("--landmarks", type=int, default=20)
