@@ -1536,31 +1536,26 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
         return;
     }
     const int D = T + 1;
+    // explicit draws, or the parity stream's draws resolved by the resolve kernel, are read where
+    // they lie (no LDS copy: beside the producer, whose workgroups hold most of each CU's LDS,
+    // every KiB of ours is residency); Philox draws are generated into LDS
+    const int32_t *dr = draws;
     if (HYP == LSLAM_HYP_PHILOX) {
         philox_draws((uint32_t)N, (uint32_t)D, (uint32_t)c, a.philox_seed, draws, lane);
         if (B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = draws[i];
     } else {
-        // explicit draws, or the parity stream's draws resolved by resolve_kernel
         const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
-        if (2 * D <= 256 && N <= 128 && B.xy) {
-            // C3-sized chunk: the draws' and the points' loads in flight together (one memory
-            // latency instead of one per copy loop), then into LDS
-            int32_t dv[4];
+        dr = h;
+        if (N <= 128 && B.xy) {
             double2 pv[2];
             const double2 *src = (const double2 *)B.xy + p0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) dv[k] = (lane + 64 * k < 2 * D) ? h[lane + 64 * k] : 0;
-#pragma unroll
             for (int k = 0; k < 2; k++) pv[k] = (lane + 64 * k < N) ? src[lane + 64 * k] : make_double2(0.0, 0.0);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (lane + 64 * k < 2 * D) draws[lane + 64 * k] = dv[k];
 #pragma unroll
             for (int k = 0; k < 2; k++)
                 if (lane + 64 * k < N) P[lane + 64 * k] = pv[k];
         } else {
-            for (int i = lane; i < 2 * D; i += 64) draws[i] = h[i];
             stage_points(B, p0, N, P, lane);
         }
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
@@ -1571,7 +1566,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     __syncthreads();
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
-    const ChunkOut o = chunk_consensus(a, P, gP, N, draws, cnt, tied, tsum, inl, vtmp, vstack, nstack,
+    const ChunkOut o = chunk_consensus(a, P, gP, N, dr, cnt, tied, tsum, inl, vtmp, vstack, nstack,
                                        B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane, chdbg);
     CH_STAMP_DECL_RESET
     const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
@@ -2724,7 +2719,7 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int T = k.T;
     int off = 0;
     k.off_pts = off; off += align16(16 * N);
-    k.off_draws = off; off += align16(8 * (T + 1));
+    k.off_draws = off; off += (k.hyp_source == LSLAM_HYP_PHILOX) ? align16(8 * (T + 1)) : 0;  // else read in place
     k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tsum = off;  // tie sums, then the inlier list
