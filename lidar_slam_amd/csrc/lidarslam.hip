@@ -558,7 +558,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
                     cm &= cm - 1ull;
                     const int t = uni(tied[kb + bit]);
                     const Model m = model2(P[draws[2 * t]], P[draws[2 * t + 1]]);
-                    const double s = pw_sum_lanes(P, N, m, vtmp, lane);
+                    const double s = pw_sum_regs(P, N, m, lane);
                     if (M > bcnt || (M == bcnt && s < bsum)) {
                         best = t;
                         bcnt = M;
@@ -2728,7 +2728,7 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     k.off_mask = off; off += align16(N);
     k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
     k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
-    k.off_vtmp = off; off += (N <= 128) ? align16(8 * 128) : 0;
+    k.off_vtmp = off;  // (pairwise sums from registers: pw_sum_regs)
     lds = off;
     if (lds > 160 * 1024) return set_err(LSLAM_ERR_CAPACITY, "chunk/trial sizes exceed the 160 KiB LDS");
     return LSLAM_OK;

@@ -251,6 +251,34 @@ __device__ __forceinline__ double pw_sum_lanes(const double2 *P, int N, const Mo
     return res;
 }
 
+// The same sum without the LDS scratch (chunk_consensus: beside the producer every KiB of LDS
+// is residency): the squared residuals stay in the lanes (point p in lane p, p + 64 in lane p's
+// second register) and the accumulators read them by shuffles, in the same order and with the
+// same tree, so the result is bit-identical to pw_sum_lanes.
+__device__ __forceinline__ double pw_sum_regs(const double2 *P, int N, const Model &m, int lane) {
+    const double v0 = lane < N ? r2sq(P[lane], m) : 0.0;
+    const double v1 = lane + 64 < N ? r2sq(P[lane + 64], m) : 0.0;
+    if (N < 8) {
+        double res = 0.0;
+        for (int i = 0; i < N; i++) res += __shfl(v0, i);
+        return res;
+    }
+    const int lim = N - (N % 8);
+    const int j = lane & 7;
+    double r = __shfl(v0, j);  // lanes 0..7: r_j = v_j + v_{j+8} + ... (i < lim), in order
+    for (int t = 1; 8 * t < lim; t++) {
+        const int i = j + 8 * t;
+        const double vi = (t < 8) ? __shfl(v0, i) : __shfl(v1, i - 64);  // t < 8 <=> i < 64 for every j
+        r += (i < lim) ? vi : 0.0;  // + 0.0 is exact (r >= 0)
+    }
+    r += __shfl_xor(r, 1);
+    r += __shfl_xor(r, 2);
+    r += __shfl_xor(r, 4);
+    double res = unid(r);
+    for (int i = lim; i < N; i++) res += (i < 64) ? __shfl(v0, i) : __shfl(v1, i - 64);
+    return res;
+}
+
 // pw_sum for any n with lanes over points: the leaves (<= 128 points) by
 // pw_sum_lanes, combined in numpy's recursion order (n2 = n/2 - (n/2)%8).
 // The node stack (nstack, 3*24 ints) and the partial sums (vst, 24 doubles)
