@@ -184,3 +184,28 @@ def test_walk_resolve_ragged_chunks(ctx, top):
             ref = np.array([st.choice2(nc) for _ in range(trials + 1)])
             assert np.array_equal(draws[c], ref), (top, s, c, nc)
         assert np.array_equal(state[s, :624], st.key) and state[s, 624] == st.pos.value
+
+
+def test_register_resolve_ragged_pipeline(ctx):
+    """The pipeline's resolve from registers (u8 steps that would fit the 16 KiB stage, the next
+    call's producer beside it): chunks of 3..256 points in one batch (K from 2, tail-only rows, to
+    fifteen 16-step loads), random points (no early stop): every chunk's draws equal the oracle's
+    choice(N, 2) sequence chained through the scan."""
+    from lidar_slam_amd.pipeline import ScanPipeline
+    sizes = [3, 4, 17, 18, 19, 33, 100, 128, 129, 200, 256]
+    S, T = 3, 60  # 61 draws x 255 steps < 16 KiB
+    sco = (np.arange(S + 1) * len(sizes)).astype(np.int32)
+    cpo = np.concatenate([[0], np.cumsum(sizes * S)]).astype(np.int32)
+    rng = np.random.default_rng(11)
+    xy = rng.uniform(-5000.0, 5000.0, (int(cpo[-1]), 2))
+    seeds = np.arange(S, dtype=np.uint32) + 9100
+    p = ScanPipeline(ctx, xy, sco, cpo, seeds=seeds, max_trials=T, want_draws=True)
+    p.run()
+    r = p.results()
+    assert not np.any(r["models"]["flags"] & 16)  # LSLAM_EARLY_STOP
+    for s in range(S):
+        st = orc.MTState(seed=int(seeds[s]))
+        for c in range(sco[s], sco[s + 1]):
+            nc = int(cpo[c + 1] - cpo[c])
+            ref = np.array([st.choice2(nc) for _ in range(T + 1)])
+            assert np.array_equal(r["draws"][c], ref), (s, c, nc)
