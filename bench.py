@@ -182,7 +182,48 @@ def load_traffic(path):
 C4_FIELDS = ("mask", "models", "ukf_x", "ukf_P", "lmk_count")
 
 
-def c4_leg(args, rank, world, dist, ctx, L):
+C4_TIMEOUT_RC = 3  # exit status of a rank whose C4 leg timed out
+
+
+def run_guarded(leg, timeout, rank, line):
+    """Run ``leg(segments)`` under a watchdog.  ``segments`` is a list the leg appends its
+    shared-memory segments to.  If the leg has not returned after ``timeout`` seconds (a hung
+    collective), rank 0 prints ``line`` with ``"c4": {"error": "timeout..."}``, unlinks the
+    segments, and the process exits with ``C4_TIMEOUT_RC`` without running further Python
+    (the hung thread cannot be joined).  A leg that raises is reported as ``{"error": ...}``."""
+    import threading
+    done, lock, segments = threading.Event(), threading.Lock(), []
+
+    def watchdog():
+        if done.wait(timeout):
+            return
+        with lock:
+            if done.is_set():
+                return
+            if rank == 0:
+                print(json.dumps(dict(line, c4={"error": "timeout: the C4 leg did not finish in %.0f s" % timeout})),
+                      flush=True)
+                for shm in segments:
+                    try:
+                        shm.unlink()
+                    except Exception:  # already gone
+                        pass
+            sys.stderr.write("bench.py: the C4 leg timed out after %.0f s; exiting %d\n" % (timeout, C4_TIMEOUT_RC))
+            sys.stderr.flush()
+            sys.stdout.flush()
+            os._exit(C4_TIMEOUT_RC)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        res = leg(segments)
+    except Exception as e:
+        res = {"error": "%s: %s" % (type(e).__name__, e)}
+    with lock:
+        done.set()
+    return res
+
+
+def c4_leg(args, rank, world, dist, ctx, L, segments=None):
     """BASELINE configs[3] (C4): ONE host batch of ``--c4-scans`` scans split across the ranks,
     end to end.  The batch lives in one shared-memory segment of the node (the stand-in for
     the reference's mp.Queue hand-off, SLAM.py:13,18-23): rank 0 creates it, each rank fills
@@ -218,6 +259,8 @@ def c4_leg(args, rank, world, dist, ctx, L):
         if rank == 0:
             try:
                 shm = shared_memory.SharedMemory(name=seg_name, create=True, size=off)
+                if segments is not None:
+                    segments.append(shm)  # unlinked by run_guarded's watchdog on a timeout
             except Exception as e:  # e.g. /dev/shm smaller than the batch
                 err = e
         if dist is not None:
@@ -531,32 +574,11 @@ def main():
         ctx.sync()
         out["philox_scans_per_s"] = round(S * args.steps / (time.perf_counter() - t0), 1)
     if args.c4 or (world > 1 and not args.no_c4):
-        # The main line stands on its own: a C4 leg that fails is reported in it, and one that
-        # does not finish in --c4-timeout seconds (a collective that never completes on some
-        # node) ends every rank with the main line printed and the leg marked as timed out.
-        import threading
-
-        done, lock = threading.Event(), threading.Lock()
-
-        def watchdog():
-            if not done.wait(args.c4_timeout):
-                with lock:
-                    if done.is_set():
-                        return
-                    if rank == 0:
-                        line = dict(out, c4={"error": "timeout: the C4 leg did not finish in %.0f s" % args.c4_timeout})
-                        print(json.dumps(line), flush=True)
-                    sys.stderr.flush()
-                    os._exit(0)
-
-        threading.Thread(target=watchdog, daemon=True).start()
-        try:
-            c4 = c4_leg(args, rank, world, dist, ctx, L)
-        except Exception as e:
-            c4 = {"error": "%s: %s" % (type(e).__name__, e)}
-        with lock:
-            done.set()
-        out["c4"] = c4
+        # The main line stands on its own: a C4 leg that fails is reported in it; one that does
+        # not finish in --c4-timeout seconds (a collective that never completes on some node)
+        # ends every rank non-zero, with the main line printed and the leg marked as timed out.
+        out["c4"] = run_guarded(lambda segs: c4_leg(args, rank, world, dist, ctx, L, segs), args.c4_timeout,
+                                rank, out)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -176,11 +176,12 @@ def _check_abi(L):
     would silently ignore appended struct fields."""
     global _err
     ver = L.lslam_version().decode(errors="replace")
-    m = re.search(r"\(abi (\d+),", ver)
+    m = re.search(r"\(abi (\d+), src ([0-9a-f]{16}),", ver)
     if not m or int(m.group(1)) != ABI_VERSION:
         _err = HIPLibraryError("%s reports %r; this binding needs ABI %d (rebuild the library)"
                                % (LIB_PATH, ver, ABI_VERSION))
         raise _err
+    _check_source(m.group(2))
     got = (C.c_int64 * 7)()
     L.lslam_abi_sizes(got, 7)
     want = [C.sizeof(t) for t in (ChunkModel, LandmarkRec, RansacParams, UkfParams, ScanBatch, ExpressMeasures,
@@ -188,6 +189,22 @@ def _check_abi(L):
     if list(got) != want:
         _err = HIPLibraryError("struct sizes differ between %s %s and the ctypes layouts %s"
                                % (LIB_PATH, list(got), want))
+        raise _err
+
+
+def _check_source(lib_hash, want=None):
+    """The library must be built from the sources next to it: a stale .so (built from other
+    sources, e.g. an A/B leftover) raises.  ``LSLAM_ALLOW_STALE=1`` skips the check (A/B runs of
+    deliberately different builds via LSLAM_LIB)."""
+    global _err
+    if os.environ.get("LSLAM_ALLOW_STALE") == "1":
+        return
+    if want is None:
+        from . import build
+        want = build.source_hash()
+    if lib_hash != want:
+        _err = HIPLibraryError("%s was built from other sources (src %s, the tree's is %s): rebuild with "
+                               "`python -m lidar_slam_amd.build`" % (LIB_PATH, lib_hash, want))
         raise _err
 
 

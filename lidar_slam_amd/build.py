@@ -5,7 +5,9 @@ reference's rounding has FMAs only where the kernels write __builtin_fma).
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -24,17 +26,40 @@ def _deps():
     return files
 
 
+def source_hash():
+    """16 hex digits of sha256 over the library's sources (csrc/*.hip, csrc/*.h,
+    include/lidarslam.h), by file name then content.  Embedded in lslam_version() so that
+    the loader can refuse a library built from other sources."""
+    h = hashlib.sha256()
+    for f in sorted(_deps(), key=os.path.basename):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path=OUT):
+    """The source hash a built library carries (None if absent or unreadable)."""
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"\(abi \d+, src ([0-9a-f]{16}),", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
 def up_to_date():
-    if not os.path.exists(OUT):
-        return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(f) <= t for f in _deps())
+    return os.path.exists(OUT) and embedded_hash(OUT) == source_hash()
+
+
+def _hash_flag():
+    return ['-DLSLAM_SRC_HASH="%s"' % source_hash()]
 
 
 def build(force=False, verbose=True):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC] + FLAGS + _hash_flag() + ["-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
@@ -45,7 +70,7 @@ def build(force=False, verbose=True):
 def build_stamps():
     """Diagnostic build with s_memtime phase stamps (tools/stamps.py)."""
     out = os.path.join(HERE, "liblidarslam_stamps.so")
-    subprocess.check_call([HIPCC] + FLAGS + ["-DLSLAM_STAMPS", "-o", out, SRC])
+    subprocess.check_call([HIPCC] + FLAGS + _hash_flag() + ["-DLSLAM_STAMPS", "-o", out, SRC])
     return out
 
 

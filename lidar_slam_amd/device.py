@@ -21,6 +21,7 @@ class Context:
         _lib.check(L.lslam_ctx_create(int(device), C.byref(h)), "lslam_ctx_create(%d)" % device)
         self.handle = h
         self.device = int(device)
+        self._inflight = []  # host buffers of async copies, held until the next sync()
 
     @staticmethod
     def device_count() -> int:
@@ -30,6 +31,7 @@ class Context:
 
     def sync(self):
         _lib.check(self._L.lslam_sync(self.handle), "lslam_sync")
+        self._inflight.clear()
 
     def set_timing(self, on: bool = True, kernels=None):
         """HIP-event timing of the kernel ids in ``kernels`` (default: all)."""
@@ -105,6 +107,7 @@ class DeviceArray:
             raise ValueError("upload size mismatch %d != %d" % (arr.nbytes, self.nbytes))
         _lib.check(self.ctx._L.lslam_h2d(self.ctx.handle, self.ptr, arr.ctypes.data_as(C.c_void_p),
                                          self.nbytes), "lslam_h2d")
+        self.ctx._inflight.append(arr)  # a caller's temporary must outlive the copy
         self.ctx.sync()  # arr may be a temporary: finish before it is freed
 
     def upload_async(self, arr):
@@ -124,6 +127,7 @@ class DeviceArray:
             raise ValueError("download_async needs a C-contiguous host array of %d bytes" % self.nbytes)
         _lib.check(self.ctx._L.lslam_d2h(self.ctx.handle, out.ctypes.data_as(C.c_void_p), self.ptr, self.nbytes),
                    "lslam_d2h")
+        self.ctx._inflight.append(out)
 
     def download(self, out=None):
         if out is None:

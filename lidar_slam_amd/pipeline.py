@@ -171,8 +171,9 @@ class ScanPipeline:
     def upload_async(self, **arrays):
         """Refresh inputs on the device without a host sync (a new batch of the same shape):
         xy / theta_deg / dist_mm / seeds / ukf_u / ukf_z / ukf_lmk by name, and ukf_x / ukf_P
-        (the filters' start state).  The host arrays must stay alive and unchanged until the
-        next sync; page-locked ones (device.register_host) copy at PCIe rate."""
+        (the filters' start state).  The host arrays must stay unchanged until the next
+        ``ctx.sync()``; converted copies (another dtype, a strided view, a list) are held by the
+        context until then.  Page-locked arrays (device.register_host) copy at PCIe rate."""
         for k, v in arrays.items():
             dst = {"ukf_x": getattr(self, "ukf_x", None), "ukf_P": getattr(self, "ukf_P", None)}.get(k) or \
                 self.inputs.get(k)

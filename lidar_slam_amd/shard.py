@@ -32,6 +32,11 @@ def shard_range(n_scans: int, world: int, rank: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+# per-scan inputs (first axis = scans); the names ScanPipeline / bench.py's C4 leg use
+PER_SCAN = frozenset(("seeds", "poses", "mt_state", "id_base", "landmarks", "lmk_count",
+                      "ukf_x", "ukf_P", "ukf_u", "ukf_z", "ukf_lmk", "x", "P", "u", "z", "lmk"))
+
+
 @dataclass
 class Shard:
     rank: int
@@ -48,7 +53,9 @@ class Shard:
 
     def inputs(self, batch):
         """The shard's slice of a host batch: xy / theta / dist by points, CSR rebased,
-        per-scan arrays (seeds, poses, UKF inputs) by scans; other entries unchanged."""
+        the per-scan arrays named in ``PER_SCAN`` (seeds, poses, MT states, UKF inputs, landmark
+        lists) by scans; every other entry (e.g. ``ukf_R_diag``, whose length 2L may equal the
+        scan count) unchanged."""
         sco, cpo = batch["scan_chunk_off"], batch["chunk_pt_off"]
         out = {}
         for k, v in batch.items():
@@ -58,7 +65,9 @@ class Shard:
                 out[k] = (cpo[self.c0:self.c1 + 1] - self.p0).astype(np.int32)
             elif k in ("xy", "theta_deg", "dist_mm"):
                 out[k] = v[self.p0:self.p1]
-            elif isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == len(sco) - 1:
+            elif k in PER_SCAN:
+                if v.shape[0] != len(sco) - 1:
+                    raise ValueError("per-scan input %r has %d rows for %d scans" % (k, v.shape[0], len(sco) - 1))
                 out[k] = v[self.lo:self.hi]
             else:
                 out[k] = v

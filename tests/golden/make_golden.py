@@ -32,10 +32,13 @@ import time
 import types
 import warnings
 
-import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import blaspin  # noqa: E402  (pins OPENBLAS_CORETYPE; must precede numpy)
+import numpy as np  # noqa: E402
 
 REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.environ.get("LSLAM_GOLDEN_OUT", HERE)  # the dispatch census writes elsewhere
 sys.path.insert(0, REF)
 sys.path.insert(0, os.path.abspath(os.path.join(HERE, "..", "..")))
 
@@ -221,7 +224,7 @@ def gen_batch(n_scans=24):
     out = rec.arrays()
     out.update(xy=b["xy"], scan_chunk_off=b["scan_chunk_off"], chunk_pt_off=b["chunk_pt_off"],
                seeds=np.asarray(ids, np.uint32))
-    np.savez_compressed(os.path.join(HERE, "batch.npz"), **out)
+    blaspin.save_npz(os.path.join(OUT, "batch.npz"), **out)
     print("batch.npz", out["xy"].shape, len(out["a"]), "chunks")
 
 
@@ -289,8 +292,8 @@ def gen_batch256(n_scans=256):
         lm_out_off=np.asarray(lout_off, np.int32), lm_out_id=np.asarray(lout_id, np.int32),
         lm_out_life=np.asarray(lout_life, np.int32),
         state_after_hash=np.asarray(state_hash, np.uint64))
-    np.savez_compressed(os.path.join(HERE, "batch256.npz"), **out)
-    print("batch256.npz", len(out["a"]), "chunks,", os.path.getsize(os.path.join(HERE, "batch256.npz")), "bytes;",
+    blaspin.save_npz(os.path.join(OUT, "batch256.npz"), **out)
+    print("batch256.npz", len(out["a"]), "chunks,", os.path.getsize(os.path.join(OUT, "batch256.npz")), "bytes;",
           "matches:", int((out["new_landmark"] == 0).sum()))
 
 
@@ -312,7 +315,7 @@ def gen_live(n_scans=14, seed=20240611):
     out = rec.arrays()
     out.update(xy=b["xy"], scan_chunk_off=b["scan_chunk_off"], chunk_pt_off=b["chunk_pt_off"],
                seed=np.asarray([seed], np.uint32))
-    np.savez_compressed(os.path.join(HERE, "live.npz"), **out)
+    blaspin.save_npz(os.path.join(OUT, "live.npz"), **out)
     print("live.npz", len(out["a"]), "chunks; matches:", int((out["new_landmark"] == 0).sum()),
           "max list", int(np.diff(out["lm_off"]).max()))
 
@@ -339,7 +342,7 @@ def gen_mt_choice():
             st = rs.get_state()
             after_key[i, j] = st[1]
             after_pos[i, j] = st[2]
-    np.savez_compressed(os.path.join(HERE, "mt_choice.npz"), seeds=seeds, ns=ns,
+    blaspin.save_npz(os.path.join(OUT, "mt_choice.npz"), seeds=seeds, ns=ns,
                         init_key=np.asarray(keys, np.uint32), words=np.asarray(words, np.uint32),
                         draws=draws, after_key=after_key, after_pos=after_pos)
     print("mt_choice.npz")
@@ -422,8 +425,8 @@ def gen_edge():
         ndraw.append(nd)
         keys.append(st[1])
         poss.append(st[2])
-    np.savez_compressed(
-        os.path.join(HERE, "edge.npz"), names=np.asarray(names), xy=np.concatenate(xy).astype(np.float64),
+    blaspin.save_npz(
+        os.path.join(OUT, "edge.npz"), names=np.asarray(names), xy=np.concatenate(xy).astype(np.float64),
         off=np.asarray(offs, np.int32), thr=np.asarray(thr), trials=np.asarray(trials, np.int32),
         seeds=np.asarray(seeds, np.uint32), err=np.asarray(err, np.int32),
         mask=np.concatenate(mask), params=np.asarray(params), ndraw=np.asarray(ndraw, np.int32),
@@ -439,7 +442,7 @@ def gen_edge():
     out = rec.arrays()
     out.update(xy=np.concatenate(seq), chunk_pt_off=np.cumsum([0] + [len(d) for d in seq]).astype(np.int32),
                scan_chunk_off=np.array([0, 3], np.int32), seed=np.array([77], np.uint32))
-    np.savez_compressed(os.path.join(HERE, "edge_chain.npz"), **out)
+    blaspin.save_npz(os.path.join(OUT, "edge_chain.npz"), **out)
     print("edge_chain.npz stop trials", out["stop_trial"], "used", out["draws_used"])
 
 
@@ -515,7 +518,7 @@ def gen_assoc():
         out[nm + "_b"] = np.asarray(d["b"], np.float64)
         out[nm + "_pos"] = np.asarray(d["pos"], np.float64).reshape(-1, 2)
         out[nm + "_end"] = np.asarray(d["end"], np.float64).reshape(-1, 2)
-    np.savez_compressed(os.path.join(HERE, "assoc.npz"), **out)
+    blaspin.save_npz(os.path.join(OUT, "assoc.npz"), **out)
     print("assoc.npz", dict(zip(names, new)), np.diff(out["lm_out_off"]))
 
 
@@ -540,7 +543,7 @@ def gen_big(n_calls=2, n_pts=4096, trials=2048):
         bt, _ = best_trial(cnt, sm)
         bests.append(bt)
         print("big", k, "inliers", m.sum(), "best", bt, "ties", int((cnt == cnt.max()).sum()))
-    np.savez_compressed(os.path.join(HERE, "big.npz"), xy=np.concatenate(xy_all), off=np.asarray(off, np.int32),
+    blaspin.save_npz(os.path.join(OUT, "big.npz"), xy=np.concatenate(xy_all), off=np.asarray(off, np.int32),
                         seeds=np.array([500 + k for k in range(n_calls)], np.uint32), trials=np.int32(trials),
                         mask=np.concatenate(masks), params=np.asarray(params), ndraw=np.asarray(ndraw, np.int32),
                         after_key=np.asarray(keys, np.uint32), after_pos=np.asarray(poss, np.int32),
@@ -556,7 +559,7 @@ def gen_known():
     res_model.params = (np.array([0.0, 0.0]), np.array([0.0, 1.0]))
     res_pts = np.array([[0.0, 0.0], [0.0, 1.0], [10.0, 0.0], [-30.0, 5.0]])
     res = res_model.residuals(res_pts)
-    np.savez_compressed(os.path.join(HERE, "known.npz"), doc_xy=np.stack([x, y], -1),
+    blaspin.save_npz(os.path.join(OUT, "known.npz"), doc_xy=np.stack([x, y], -1),
                         doc_origin=lm.params[0], doc_direction=lm.params[1],
                         res_pts=res_pts, res_params=np.array([0.0, 0.0, 0.0, 1.0]), res=res)
     print("known.npz", lm.params, res)

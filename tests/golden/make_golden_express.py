@@ -27,10 +27,13 @@ import os
 import sys
 import types
 
-import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import blaspin  # noqa: E402  (pins OPENBLAS_CORETYPE; must precede numpy)
+import numpy as np  # noqa: E402
 
 REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.environ.get("LSLAM_GOLDEN_OUT", HERE)  # the dispatch census writes elsewhere
 sys.path.insert(0, REF)
 sys.modules["serial"] = types.ModuleType("serial")  # only the port methods use it
 
@@ -213,7 +216,7 @@ def main():
     for name, r in caps.items():
         for k, v in r.items():
             flat["%s_%s" % (name, k)] = v
-    np.savez_compressed(os.path.join(HERE, "express.npz"), **flat)
+    blaspin.save_npz(os.path.join(OUT, "express.npz"), **flat)
     print("express.npz:", {k: v.shape for k, v in flat.items()})
 
 

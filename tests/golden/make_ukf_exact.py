@@ -18,9 +18,12 @@ import os
 import sys
 import time
 
-import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import blaspin  # noqa: E402  (pins OPENBLAS_CORETYPE; must precede numpy)
+import numpy as np  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.environ.get("LSLAM_GOLDEN_OUT", HERE)  # the dispatch census writes elsewhere
 ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
 sys.path.insert(0, ROOT)
 
@@ -76,8 +79,8 @@ def main():
     x, lmk, z = _filters(rng, S, L)
     out.update(case("predict", x, np.tile(np.diag([.1, .1, .05]), (S, 1, 1)), np.tile([2.0, 2.5], (S, 1)), z, lmk,
                     np.array([oukf.VAR_DIST, oukf.VAR_ANGLE] * L), update=False))
-    np.savez_compressed(os.path.join(HERE, "ukf_exact.npz"), **out)
-    print("ukf_exact.npz", os.path.getsize(os.path.join(HERE, "ukf_exact.npz")), "bytes")
+    blaspin.save_npz(os.path.join(OUT, "ukf_exact.npz"), **out)
+    print("ukf_exact.npz", os.path.getsize(os.path.join(OUT, "ukf_exact.npz")), "bytes")
 
 
 if __name__ == "__main__":

@@ -38,6 +38,27 @@ def test_struct_layouts():
         assert getattr(_lib.ChunkModel, f).offset == pl.MODEL_DTYPE.fields[f][1]
 
 
+def test_library_built_from_these_sources():
+    from lidar_slam_amd import build
+    L = _lib.load()
+    assert ("src %s," % build.source_hash()).encode() in L.lslam_version()
+    assert build.embedded_hash() == build.source_hash()
+
+
+def test_stale_library_raises(monkeypatch):
+    """A library whose embedded source hash differs from the tree's is refused (no silent A/B leftovers)."""
+    from lidar_slam_amd import build
+    monkeypatch.delenv("LSLAM_ALLOW_STALE", raising=False)
+    monkeypatch.setattr(_lib, "_err", None)
+    with pytest.raises(_lib.HIPLibraryError, match="built from other sources"):
+        _lib._check_source("0123456789abcdef", want=build.source_hash())
+    with pytest.raises(_lib.HIPLibraryError, match="built from other sources"):
+        _lib._check_source("0123456789abcdef")
+    _lib._check_source(build.source_hash())
+    monkeypatch.setenv("LSLAM_ALLOW_STALE", "1")
+    _lib._check_source("0123456789abcdef")
+
+
 def test_version_and_defaults():
     L = _lib.load()
     assert b"gfx950" in L.lslam_version()

@@ -391,6 +391,51 @@ def test_ukf_vs_oracle(ctx):
     _ukf_close(r["ukf_x"], r["ukf_P"], xo, Po)
 
 
+@pytest.mark.parametrize("L,lanes", [(20, "1"), (20, "0"), (4, "1")])
+def test_fused_ukf_landmarks_from_ransac_vs_oracle(ctx, L, lanes, monkeypatch):
+    """flags = PREDICT | UPDATE | LMK_FROM_RANSAC in the fused pipeline: landmark slot j of
+    scan s becomes chunk j's fitted origin (Landmark.pos, ransac_functions.py:31) wherever that
+    chunk is LSLAM_VALID, the rest keep ukf_lmk.  The kernel's (x, P) must equal the oracle's UKF
+    run on exactly that substituted landmark set (1e-5 per component).  L = 4 < 8 chunks: only
+    the first L chunks feed slots.  Both UKF forms (lane groups, one wave per scan)."""
+    from lidar_slam_amd.pipeline import ScanPipeline
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.device import Context
+    from oracle import ukf as oukf
+    monkeypatch.setenv("LSLAM_UKF_LANES", lanes)  # read when a context is created
+    ctx = Context(0)
+    ids = list(range(40))
+    b = synth.make_batch(ids)
+    S = len(ids)
+    rng = np.random.default_rng(17)
+    lmk = rng.uniform(-3000, 3000, (S, L, 2))
+    x = b["poses"].copy()
+    z = np.stack([oukf.transfer_function(x[s], lmk[s]) for s in range(S)]) + rng.normal(0, 0.3, (S, 2 * L))
+    P = np.tile(np.diag([.1, .1, .05]), (S, 1, 1))
+    u = np.tile([2.0, 2.5], (S, 1))
+    Rd = np.array([oukf.VAR_DIST, oukf.VAR_ANGLE] * L)
+    p = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids), lmk_capacity=32,
+                     ukf=dict(n_landmarks=L, x=x, P=P, u=u, z=z, lmk=lmk, R_diag=Rd, flags=7))
+    p.run()
+    r = p.results()
+    m = r["models"]
+    sco = b["scan_chunk_off"]
+    lmk2 = lmk.copy()
+    replaced = 0
+    for s in range(S):
+        for j in range(min(L, sco[s + 1] - sco[s])):
+            c = sco[s] + j
+            if m["flags"][c] & 1:
+                lmk2[s, j] = (m["ox"][c], m["oy"][c])
+                replaced += 1
+    assert replaced >= S * min(L, 8) * 0.9
+    xo, Po = oukf.ukf_batch(x, P, u, z, lmk2, Rd)
+    _ukf_close(r["ukf_x"], r["ukf_P"], xo, Po)
+    # and it is not the un-substituted step
+    xn, _ = oukf.ukf_batch(x, P, u, z, lmk, Rd)
+    assert np.max(np.abs(r["ukf_x"] - xn)) > 1e-3
+
+
 def _border_batch():
     """Chunks whose residuals sit on the inlier threshold (r^2 within ulps of
     the cutoff, where the consensus kernel's cheap cross-product test defers to

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 
 from lidar_slam_amd import shard
 from lidar_slam_amd.pipeline import LANDMARK_DTYPE, MODEL_DTYPE
@@ -37,6 +38,22 @@ def test_plan_inputs_rebase():
         assert np.array_equal(sub["seeds"], np.array(ids[sh.lo:sh.hi], np.uint32))
         assert np.array_equal(sub["ukf_x"], batch["ukf_x"][sh.lo:sh.hi])
         assert np.array_equal(sub["ukf_R_diag"], batch["ukf_R_diag"])  # not per scan
+
+
+def test_inputs_do_not_slice_r_diag_when_2l_equals_scans():
+    """R_diag has 2L entries; with 2L == the scan count it must still pass through whole."""
+    import bench
+    ids = list(range(8))
+    b, ukf = bench.make_workload(ids, 720, 4)   # L = 4 -> R_diag has 8 = n_scans entries
+    batch = dict(b, seeds=np.array(ids, np.uint32), **{"ukf_" + k: v for k, v in ukf.items() if k != "n_landmarks"})
+    assert batch["ukf_R_diag"].shape[0] == len(ids)
+    for sh in shard.plan(b["scan_chunk_off"], b["chunk_pt_off"], 3):
+        sub = sh.inputs(batch)
+        assert np.array_equal(sub["ukf_R_diag"], batch["ukf_R_diag"])
+        assert np.array_equal(sub["ukf_z"], batch["ukf_z"][sh.lo:sh.hi])
+    bad = dict(batch, seeds=np.arange(5, dtype=np.uint32))
+    with pytest.raises(ValueError, match="per-scan input 'seeds'"):
+        shard.plan(b["scan_chunk_off"], b["chunk_pt_off"], 2)[0].inputs(bad)
 
 
 def _oracle_results(b, ids, ukf, cap):

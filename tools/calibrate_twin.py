@@ -27,6 +27,8 @@ import types
 
 os.environ["OPENBLAS_NUM_THREADS"] = "1"
 os.environ["OMP_NUM_THREADS"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden"))
+import blaspin  # noqa: E402  (pins OPENBLAS_CORETYPE = SkylakeX; must precede numpy)
 import numpy as np  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -98,6 +100,7 @@ def main():
         "twin_over_reference": round(t_ref / t_twin, 3),
         "cores": 1, "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
         "python": platform.python_version(), "numpy": np.__version__,
+        "blas_core": str(blaspin.meta()["meta_blas_core"]),
         "note": "reference = ransac_functions.landmark_extraction (skimage 0.18.3 ransac) per chunk as check_ransac "
                 "drives it; twin = oracle/numpy_twin.process_scan; same scans and seeds, inlier counts equal",
     }
