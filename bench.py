@@ -79,15 +79,21 @@ def make_workload(scan_ids, n_beams, L, seed_base=0):
     return b, ukf
 
 
-def _twin_worker(args):
-    xy, cpo, seed, ukf_in = args
-    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+_TWIN_JOBS = None  # set before the pool forks: the workers inherit the sample, only indices travel
+
+
+def _twin_run(job):
+    xy, cpo, seed, ukf_in = job
     from oracle import numpy_twin as tw
     from oracle import ukf as oukf
     tw.process_scan(xy, cpo, seed)
     x, P, u, z, lmk, Rd = ukf_in
     oukf.ukf_batch(x[None], P[None], u[None], z[None], lmk[None], Rd)
     return 1
+
+
+def _twin_worker(rng):
+    return sum(_twin_run(_TWIN_JOBS[i]) for i in range(*rng))
 
 
 def _twin_jobs(n_scans, n_beams, L):
@@ -105,10 +111,10 @@ def _twin_jobs(n_scans, n_beams, L):
 def cpu_baseline_1core(n_scans, n_beams, L):
     """The same twin in this process alone: one core (OPENBLAS_NUM_THREADS=1 is set at import)."""
     jobs = _twin_jobs(n_scans, n_beams, L)
-    _twin_worker(jobs[0])
+    _twin_run(jobs[0])
     t0 = time.perf_counter()
     for j in jobs:
-        _twin_worker(j)
+        _twin_run(j)
     dt = time.perf_counter() - t0
     return len(jobs) / dt, dt
 
@@ -125,6 +131,24 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2 CPU quota
+    (cpu.max) if one is set.  Returns (cpus, quota_cpus or None)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), quota
+
+
 def capacity_overflows(models):
     """Chunks whose new landmark was dropped because the per-scan list was full (LSLAM_CAPACITY).
     The reference's list is unbounded (ransac_functions.py:75-76): a timed step is
@@ -133,16 +157,22 @@ def capacity_overflows(models):
 
 
 def cpu_baseline(n_scans, n_beams, L, procs):
-    """The reference's CPU path (NumPy twin, per-trial skimage structure) +
-    the NumPy UKF restatement, over a bounded sample, on `procs` host cores."""
+    """The reference's CPU path (NumPy twin, per-trial skimage structure) + the NumPy UKF
+    restatement, over a bounded sample, on ``procs`` host processes (one per core).  The
+    sample is made once here; the forked workers inherit it and receive index ranges."""
     import multiprocessing as mp
-    jobs = _twin_jobs(n_scans, n_beams, L)
+    global _TWIN_JOBS
+    _TWIN_JOBS = _twin_jobs(n_scans, n_beams, L)
+    n = len(_TWIN_JOBS)
+    per = max(1, n // (4 * procs))  # ~4 ranges per process: balances the tail
+    ranges = [(i, min(n, i + per)) for i in range(0, n, per)]
     ctx = mp.get_context("fork")
     with ctx.Pool(procs) as pool:
-        pool.map(_twin_worker, jobs[:procs])  # warm the workers (imports)
+        pool.map(_twin_worker, [(i % n, i % n + 1) for i in range(procs)], chunksize=1)  # warm imports
         t0 = time.perf_counter()
-        done = sum(pool.map(_twin_worker, jobs, chunksize=max(1, len(jobs) // (4 * procs))))
+        done = sum(pool.map(_twin_worker, ranges, chunksize=1))
         dt = time.perf_counter() - t0
+    _TWIN_JOBS = None
     return done / dt, dt
 
 
@@ -393,9 +423,10 @@ def main():
     ap.add_argument("--hyp", default="mt19937", choices=["mt19937", "philox"])
     ap.add_argument("--no-ukf", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="CPU baseline: at least this many scans")
+    ap.add_argument("--cpu-per-proc", type=int, default=16, help="CPU baseline: at least this many scans per process")
     ap.add_argument("--cpu-sample-1core", type=int, default=96)
-    ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default: every usable core)")
     ap.add_argument("--lmk-capacity", type=int, default=64,
                     help="per-scan landmark list capacity (>= the steady-state list, ~42 on C3)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -416,16 +447,19 @@ def main():
     # CPU baseline first: before anything touches the GPU (the pool forks)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        procs = args.cpu_procs or max(1, min(16, os.cpu_count() or 1))
+        usable, quota = usable_cpus()
+        procs = args.cpu_procs or usable
+        sample = max(args.cpu_sample, args.cpu_per_proc * procs)
         rate1, dt1 = cpu_baseline_1core(args.cpu_sample_1core, args.beams, L)
-        rate, dt = cpu_baseline(args.cpu_sample, args.beams, L, procs)
+        rate, dt = cpu_baseline(sample, args.beams, L, procs)
         cpu = {"value": round(rate, 2), "unit": "scans/s", "cores": procs, "kind": "port",
-               "value_1core": round(rate1, 2), "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+               "value_1core": round(rate1, 2), "host_cpus": os.cpu_count(), "usable_cpus": usable,
+               "cgroup_cpu_quota": quota, "cpu_model": cpu_model(),
                "sample": "%d synthetic %d-pt scans (same generator, per-scan seeds) through the NumPy twin of "
                          "the reference (skimage-structured ransac + landmark association, oracle/numpy_twin.py) "
-                         "+ the NumPy UKF restatement (oracle/ukf.py), %d processes, %.1f s wall; 1 core: %d "
-                         "scans in %.1f s; twin/reference calibration in BASELINE.md"
-                         % (args.cpu_sample, args.beams, procs, dt, args.cpu_sample_1core, dt1)}
+                         "+ the NumPy UKF restatement (oracle/ukf.py), %d processes (one per usable core), %.2f s "
+                         "wall; 1 core: %d scans in %.1f s; twin/reference calibration in BASELINE.md"
+                         % (sample, args.beams, procs, dt, args.cpu_sample_1core, dt1)}
 
     dist = None
     if world > 1:

@@ -34,9 +34,22 @@ def counter(path, name, kernel_sub="scan_kernel"):
 
 
 # kernel-name substrings: producer, consensus, fix-up (scan_kernel<MT, RANSAC>), post pass (scan_kernel<EXPLICIT, ...>)
-KERNELS = {"rng_kernel": "rng_kernel", "resolve_kernel": "resolve_kernel", "chunk_kernel": "chunk_kernel",
-           "fixup": "scan_kernel<0, 1>",
+KERNELS = {"rng_kernel": "rng_kernel", "resolve_reg_kernel": "resolve_reg_kernel", "resolve_kernel": "resolve_kernel<",
+           "chunk_kernel": "chunk_kernel", "ukf_group_kernel": "ukf_group_kernel", "fixup": "scan_kernel<0, 1>",
            "post": "scan_kernel<2, "}
+
+
+def resolve_alg_bytes(beams, scans, trials):
+    """The resolve's algorithmic bytes per launch: every Fisher-Yates step read once (u8, chunks
+    <= 256 points: D = trials + 1 draws of K = N - 1 steps per chunk) + the draws written
+    (2 x int32 per draw)."""
+    sys.path.insert(0, ROOT)
+    from lidar_slam_amd import synth
+    sizes = synth.chunk_sizes(beams)
+    D = trials + 1
+    steps = sum(D * (n - 1) for n in sizes if n >= 3)
+    draws = sum(D * 8 for n in sizes if n >= 3)
+    return scans * steps, scans * draws
 
 
 def main(tag, bench_log=None):
@@ -66,6 +79,13 @@ def main(tag, bench_log=None):
     for k, v in per.items():
         lines.append("- `%s`: FETCH_SIZE %.1f KiB, WRITE_SIZE %.1f KiB -> %d bytes/launch"
                      % (k, v["fetch_kib"], v["write_kib"], v["bytes_per_launch"]))
+    cfg = bench["config"]
+    st, dr = resolve_alg_bytes(cfg["points_per_scan"], cfg["scans_per_gpu"], cfg["trials"])
+    if "resolve_reg_kernel" in per:
+        v = per["resolve_reg_kernel"]
+        lines += ["", "Resolve, algorithmic vs PMC: steps read %d B + draws written %d B = %d B per launch; PMC read "
+                  "%d B (x2 corrected), written %d B." % (st, dr, st + dr, int(2 * v["fetch_kib"] * 1024),
+                                                         int(v["write_kib"] * 1024))]
     # the profiled process's own bench line: its HIP-event kernel time must agree with rocprof's
     scans = bench["config"]["scans_per_gpu"]
     sq = {}
