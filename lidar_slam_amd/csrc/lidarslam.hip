@@ -1345,6 +1345,75 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
     }
 }
 
+// The register walk for K <= 127 and at most 128 draws (C3), with the whole row in
+// registers before the walk starts.  resolve_reg_kernel loads 16 steps, walks them,
+// then loads the next 16: between a wave's loads the other waves of its XCD stream
+// their own rows (and the producer its steps) through the L2, so a cache line of
+// the 64 rows was fetched from HBM ~4x per launch (PMC 1.21 GB read vs 0.29 GB of
+// steps, profiles/r03a_rocprof.md).  Here a wave (one chunk, 64 draws) issues all
+// of its rows' loads (up to 8 x 16 bytes per lane) back to back, so every line of
+// its 64 rows is requested once, while it is in flight.
+// Group t of a row is bytes [K - 16(t+1), K - 16t) = steps i = 16t+1 .. 16t+16 (step
+// i at byte K - i); the lowest group may start up to 15 bytes before the row (the
+// previous row, or the slot's front pad JBUF_FRONT) and walks only i <= K.
+constexpr int RR_GROUPS = 8;  // K <= 127
+constexpr size_t JBUF_FRONT = 64;  // bytes of a producer slot before its steps
+template <bool CHECK>
+__device__ __forceinline__ void rr_walk16(const uint4 v, uint32_t t, uint32_t K, uint32_t &c0, uint32_t &c1) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        const uint32_t i = 16u * t + 1u + (uint32_t)u;  // byte 15 - u of the group
+        if (i < 2u) continue;                             // step 1: j_1 decides the final swap
+        if (CHECK && i > K) break;
+        const int off = 15 - u;
+        const uint32_t nb = 32u - (uint32_t)__clz((int)i);  // mask(i) = 2^nb - 1
+        const uint32_t j = __builtin_amdgcn_ubfe(w[off >> 2], (uint32_t)(8 * (off & 3)), nb);
+        c0 = (j == c0) ? i : c0;
+        c1 = (j == c1) ? i : c1;
+    }
+}
+
+__device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t &c0, uint32_t &c1) {
+    const uint32_t nfull = K >> 4;  // groups with all 16 steps <= K
+#pragma unroll
+    for (int t = 0; t < RR_GROUPS; t++) {
+        if ((uint32_t)t < nfull) rr_walk16<false>(w[t], (uint32_t)t, K, c0, c1);
+        else if ((uint32_t)t == nfull) rr_walk16<true>(w[t], (uint32_t)t, K, c0, c1);
+    }
+}
+
+__global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
+    const int ng = (int)((D + 63u) >> 6);  // waves per chunk: lanes = 64 draws
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
+    const int64_t total = (int64_t)B.n_chunks * ng;
+    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
+        const int c = (int)(e / ng);
+        const uint32_t d = 64u * (uint32_t)(e - (int64_t)c * ng) + (uint32_t)lane;
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        const uint32_t K = (uint32_t)N - 1u;  // <= 127 (host)
+        const uint8_t *row = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)(d < D ? d : 0u) * K;
+        uint4 w[RR_GROUPS];
+#pragma unroll
+        for (int t = 0; t < RR_GROUPS; t++)
+            if ((uint32_t)(16 * t) < K) w[t] = load16_unaligned(row + (int)K - 16 * (t + 1));
+        uint32_t c0 = 0, c1 = 1;
+        rr_walk_row(w, K, c0, c1);
+        if (d < D) {
+            const uint32_t j1 = (w[0].w >> 24) & 1u;  // byte K - 1: step 1
+            int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)(a.ep_d0 + d);
+            draws[0] = (int32_t)((j1 == 0u) ? c1 : c0);
+            draws[1] = (int32_t)((j1 == 0u) ? c0 : c1);
+        }
+    }
+}
+
 // Chunks whose steps do not fit the 16 KiB stage (C5: 2049 draws x 4095 steps
 // x 2 B = 16.8 MB per chunk).  One wave per (chunk, group of 64 draws), lanes =
 // draws as in resolve_draws_fwd, but the steps stream through an LDS tile of
@@ -2052,7 +2121,7 @@ struct lslam_ctx {
     int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
     int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
     int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
-    int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage)
+    int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage, 2: resolve_reg_kernel)
     int resolve_beside;  // this call's resolves will likely run beside the next call's producer
     int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
@@ -2199,7 +2268,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     }
     {
         const char *e = getenv("LSLAM_RESOLVE_REG");
-        c->resolve_reg = (e && atoi(e) == 0) ? 0 : 1;
+        c->resolve_reg = e ? (atoi(e) == 2 ? 2 : atoi(e) == 0 ? 0 : 1) : 1;  // 2: the 16-step walk (A/B)
     }
     c->resolve_beside = 0;
     c->timing_mask = 0xffffffffu;
@@ -2805,7 +2874,7 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     k.ep_nd = De < D ? De : 0;
     k.ep_d0 = 0;
     k.ep_count = (D + De - 1) / De;
-    const size_t jbytes = ((size_t)De * per_draw + 64 + 255) & ~(size_t)255;
+    const size_t jbytes = ((size_t)De * per_draw + JBUF_FRONT + 64 + 255) & ~(size_t)255;
     const size_t sbytes = (size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4;
     if (c->pslot_bytes < jbytes + sbytes) {
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -2822,7 +2891,7 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
         }
         c->pslot_bytes = jbytes + sbytes;
     }
-    k.jbuf = c->pslot[slot];
+    k.jbuf = (unsigned char *)c->pslot[slot] + JBUF_FRONT;
     k.state_scr = (uint32_t *)((unsigned char *)c->pslot[slot] + jbytes);
     k.slot_jbytes = jbytes;
     if (k.b.draws_out) {
@@ -2868,8 +2937,13 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         return LSLAM_OK;
     }
     if (k.j8 && c->resolve_reg && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
-        const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
-        hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, c->stream, k);
+        if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg != 2) {
+            const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 63) / 64))), block(64);
+            hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, c->stream, k);
+        } else {
+            const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
+            hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, c->stream, k);
+        }
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
@@ -2936,7 +3010,7 @@ static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint3
         if (k.ep_count > 1) {
             ke.ep_d0 = e * k.ep_nd;
             ke.ep_nd = std::min(k.ep_nd, D - ke.ep_d0);
-            ke.jbuf = c->pslot[sl];
+            ke.jbuf = (unsigned char *)c->pslot[sl] + JBUF_FRONT;
             ke.state_scr = (uint32_t *)((unsigned char *)c->pslot[sl] + k.slot_jbytes);
             if (e > 0) {
                 if (ps != c->stream) HIPCHK(hipStreamWaitEvent(ps, c->ev_slot_free[sl], 0));
