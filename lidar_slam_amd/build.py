@@ -74,8 +74,17 @@ def build_stamps():
     return out
 
 
+def build_census():
+    """Diagnostic build with only the wave census (tools/census.py): production timing."""
+    out = os.path.join(HERE, "liblidarslam_census.so")
+    subprocess.check_call([HIPCC] + FLAGS + _hash_flag() + ["-DLSLAM_CENSUS", "-o", out, SRC])
+    return out
+
+
 if __name__ == "__main__":
     if "--stamps" in sys.argv:
         build_stamps()
+    elif "--census" in sys.argv:
+        build_census()
     else:
         build(force="--force" in sys.argv)

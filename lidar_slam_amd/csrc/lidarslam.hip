@@ -144,7 +144,45 @@ struct KArgs {
     double *models;     // [n_chunks][T][4] 2-point models (origin, direction)
     int cnt_blocks;     // count_kernel workgroups per chunk
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
+    unsigned long long *wcen;  // diagnostic build only: wave census records [256][cap / 256][3] (WaveCensus)
+    unsigned int *wcen_n;      // [256] records claimed so far per bucket
+    unsigned int wcen_cap;
+    unsigned int call_seq;     // host's pipeline-call counter (census tag)
 };
+
+// Diagnostic build only (-DLSLAM_STAMPS): one record per wave of a consumer or producer
+// kernel, {kernel id | call << 8 | HW_ID << 24 | XCC_ID << 56, s_memrealtime at entry,
+// at exit} (100 MHz chip clock), for tools/census.py: when each wave of each dispatch
+// became resident, how long it lived, and on which SIMD.  The product build has none.
+enum { WC_RNG_PARSER = 1, WC_RNG_HELPER, WC_RESOLVE, WC_CHUNK, WC_FIXUP, WC_POST, WC_UKF };
+#if defined(LSLAM_STAMPS) || defined(LSLAM_CENSUS)
+struct WaveCensus {
+    const KArgs &a;
+    uint32_t kid;
+    uint64_t t0;
+    __device__ WaveCensus(const KArgs &a_, uint32_t kid_) : a(a_), kid(kid_), t0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~WaveCensus() {
+        if (!a.wcen || (threadIdx.x & 63) != 0) return;
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+        // 256 buckets of wcen_cap / 256 records, one counter each: one counter for every
+        // wave of a launch was a hot spot that slowed the consumers' last instructions
+        const unsigned int bk = (blockIdx.x * 7u + (threadIdx.x >> 6)) & 255u, per = a.wcen_cap >> 8;
+        const unsigned int i = atomicAdd(a.wcen_n + bk, 1u);
+        if (i >= per) return;
+        unsigned long long *r = a.wcen + 3 * ((size_t)bk * per + i);
+        r[0] = (uint64_t)kid | ((uint64_t)(a.call_seq & 0xffffu) << 8) | ((uint64_t)hw << 24) | ((uint64_t)xcc << 56);
+        r[1] = t0;
+        r[2] = t1;
+    }
+};
+#define WAVE_CENSUS(a, kid) WaveCensus _wave_census((a), (kid))
+#else
+#define WAVE_CENSUS(a, kid) \
+    do {                    \
+    } while (0)
+#endif
 
 // ------------------------------------------------------------------------
 // per-chunk RANSAC on one wave
@@ -1070,6 +1108,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 template <int HYP, int MODE>
 __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    WAVE_CENSUS(a, a.fixup ? WC_FIXUP : WC_POST);
     if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);
     for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
         scan_body<HYP, MODE>(a, s, smem);
@@ -1093,7 +1132,9 @@ __global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg, in
     const int lane = (int)threadIdx.x;
     const int g = lane & (Pg - 1);
     const int s = (int)blockIdx.x * (64 / Pg) + lane / Pg;
-    if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);  // the post pass's level
+    WAVE_CENSUS(a, WC_UKF);
+    const int uprio = (a.cons_prio & 256) ? (a.cons_prio >> 6) & 3 : (a.cons_prio >> 4) & 3;  // default: the post's
+    if (uprio) set_prio_level(uprio);
     if (s >= B.n_scans) return;  // whole groups only: the butterfly stays inside a group
     double x[3], Pm[9];
     for (int i = 0; i < 3; i++) x[i] = B.ukf_x[3 * (size_t)s + i];
@@ -1149,6 +1190,7 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : (uint32_t)a.T + 1u;  // draws of this launch
+    WAVE_CENSUS(a, wave < PPW ? WC_RNG_PARSER : WC_RNG_HELPER);
     auto pipe_of = [&](int j) {
         RngPipe rp;
         unsigned char *base = smem + (size_t)j * a.rng_pipe_bytes;
@@ -1389,6 +1431,7 @@ __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
     const uint32_t Dall = (uint32_t)a.T + 1u;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
     const int ng = (int)((D + 63u) >> 6);  // waves per chunk: lanes = 64 draws
+    WAVE_CENSUS(a, WC_RESOLVE);
     if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     const int64_t total = (int64_t)B.n_chunks * ng;
     for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
@@ -1650,6 +1693,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
 template <int HYP>
 __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    WAVE_CENSUS(a, WC_CHUNK);
     if ((a.cons_prio >> 2) & 3) set_prio_level((a.cons_prio >> 2) & 3);
     for (int c = blockIdx.x; c < a.b.n_chunks; c += gridDim.x) {
         chunk_body<HYP>(a, c, smem);
@@ -2121,6 +2165,7 @@ struct lslam_ctx {
     int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
     int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
     int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
+    int ukf_side_mt;   // env LSLAM_UKF_SIDE=1: an independent UKF on the side stream in parity mode too (A/B)
     int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage, 2: resolve_reg_kernel)
     int resolve_beside;  // this call's resolves will likely run beside the next call's producer
     int n_cus;         // compute units of the device
@@ -2265,6 +2310,10 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     {
         const char *e = getenv("LSLAM_UKF_LANES");
         c->ukf_lanes = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    {
+        const char *e = getenv("LSLAM_UKF_SIDE");
+        c->ukf_side_mt = (e && atoi(e) != 0) ? 1 : 0;
     }
     {
         const char *e = getenv("LSLAM_RESOLVE_REG");
@@ -2629,6 +2678,18 @@ static int validate_batch(const lslam_scan_batch *b, bool need_points) {
     return LSLAM_OK;
 }
 
+#if defined(LSLAM_STAMPS) || defined(LSLAM_CENSUS)
+static unsigned long long *g_wcen = nullptr;  // wave census (diagnostic builds)
+static unsigned int *g_wcen_n = nullptr;
+static unsigned int g_wcen_cap = 0;
+static unsigned int g_call_seq = 0;
+extern "C" int lslam_debug_set_census(unsigned long long *dev_buf, unsigned int *dev_count, unsigned int cap) {
+    g_wcen = dev_buf;
+    g_wcen_n = dev_count;
+    g_wcen_cap = cap;
+    return LSLAM_OK;
+}
+#endif
 #ifdef LSLAM_STAMPS
 static unsigned long long *g_dbg = nullptr;
 extern "C" int lslam_debug_set_stamps(unsigned long long *dev_buf) {
@@ -2643,12 +2704,23 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
 #ifdef LSLAM_STAMPS
     k.dbg = g_dbg;
 #endif
+#if defined(LSLAM_STAMPS) || defined(LSLAM_CENSUS)
+    k.wcen = g_wcen;
+    k.wcen_n = g_wcen_n;
+    k.wcen_cap = g_wcen_cap;
+    k.call_seq = g_call_seq;
+#endif
     static const int cons_prio = [] {
-        // LSLAM_CONS_PRIO="PCR": post, chunk, resolve wave priorities (digits 0-3)
-        // default "000": every consumer at the lowest level, beside the parsers' levels 3..1
-        // (measured: all consumers at 3 ran +40 %, other mixes within 1 %)
+        // LSLAM_CONS_PRIO="[U]PCR": UKF (default: = post), post, chunk, resolve wave priorities
+        // (digits 0-3); default "000": every consumer at the lowest level, beside the parsers'
+        // levels 3..1 (measured: all consumers at 3 ran +40 %)
         const char *e = getenv("LSLAM_CONS_PRIO");
-        if (!e || strlen(e) != 3) e = "000";
+        if (!e || (strlen(e) != 3 && strlen(e) != 4)) e = "000";
+        if (strlen(e) == 4) {
+            const int u = (e[0] - '0') & 3;
+            e += 1;
+            return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4) | (u << 6) | 256;
+        }
         return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4);
     }();
     k.cons_prio = cons_prio;
@@ -3225,8 +3297,10 @@ static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
         set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>);
         set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
-    const dim3 grid(launch_cap(c, k.b.n_scans));
     static const bool w4 = [] { const char *e = getenv("LSLAM_POST_W4"); return e && atoi(e) != 0; }();
+    static const int post_cap = [] { const char *e = getenv("LSLAM_POST_CAP"); return e ? atoi(e) : 0; }();
+    const int64_t cap = post_cap > 0 && k.hyp_source == LSLAM_HYP_MT19937 ? (int64_t)post_cap * 4 * c->n_cus : k.b.n_scans;
+    const dim3 grid(launch_cap(c, std::min<int64_t>(k.b.n_scans, cap)));
     if (k.hyp_source == LSLAM_HYP_MT19937 && !w4)  // beside the next call's producer
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     else
@@ -3240,6 +3314,9 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
                      const lslam_ukf_params *u) {
     HIPCHK(hipSetDevice(c->device));
     if (b->n_scans == 0) return LSLAM_OK;
+#if defined(LSLAM_STAMPS) || defined(LSLAM_CENSUS)
+    g_call_seq += 1;
+#endif
     const bool assoc = b->landmarks != nullptr;
     KArgs k;
     int lds_fix = 0;
@@ -3258,7 +3335,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     // on the side stream, off the resolve -> consensus -> association chain
     // (Philox / explicit hypotheses only: beside the MT producer a third stream of UKF waves
     // slows the resolve -> consensus chain more than it saves, 1.23 -> 1.27-1.32 ms on C3)
-    const bool ukf_side = p->hyp_source != LSLAM_HYP_MT19937 && u &&
+    const bool ukf_side = (p->hyp_source != LSLAM_HYP_MT19937 || c->ukf_side_mt) && u &&
                           !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
     // the UKF of the fused call on lane groups after the association pass (not in MAP mode,
     // whose measurements come out of the association walk itself)
@@ -3324,8 +3401,21 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         st = produce_draws(c, k, slot, c->pstream, nullptr, slot);  // slot <- the last epoch's
         if (st) return st;
     }
+    // a UKF that reads nothing of this call's RANSAC may run anywhere in the ctx chain
+    // (LSLAM_UKF_EARLY: 0 after the post pass, 1 before the fix-up, 2 before the consensus)
+    static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 0; }();
+    const bool ukf_indep = ukf_lane && !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
+    const int ukf_at = ukf_indep ? ukf_early : 0;
+    if (ukf_lane && ukf_at == 2) {
+        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
+        HIPCHK(hipGetLastError());
+    }
     st = launch_chunks(c, k, !assoc);
     if (st) return st;
+    if (ukf_lane && ukf_at == 1) {
+        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
+        HIPCHK(hipGetLastError());
+    }
     if (mt) {
         KArgs kf = k;
         kf.fixup = 1;
@@ -3347,7 +3437,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
-    if (ukf_lane) {
+    if (ukf_lane && ukf_at == 0) {
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
         HIPCHK(hipGetLastError());
     }
