@@ -130,6 +130,7 @@ struct KArgs {
     uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
     int off_blk, off_fl, off_nxt, off_vtmp, off_stage, off_tbl;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
+    int off_stbl;        // rng_kernel, shared tables (>= 0): [2] K claims then 2 tables after the pipes
     const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127 (null: mask evaluation only)
     // producer epochs (one-chunk scans whose steps exceed the slot budget): this launch
     // covers draws [ep_d0, ep_d0 + ep_nd) of every chunk; ep_nd = 0: all T + 1 draws
@@ -1200,6 +1201,53 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         rp.tblK = 0;
         return rp;
     };
+    // Shared reject tables (off_stbl >= 0): the workgroup's parsers claim up to two table Ks
+    // (K = N-1 <= RT_KMAX of their chunks) and the workgroup loads those two tables once; a
+    // chunk whose K got no slot is parsed in mask mode (same steps).  Per-parser tables held
+    // 4 x 3.5 KiB of each workgroup's LDS: ~142 of a CU's 160 KiB with 4 workgroups, which
+    // left the consumers beside the producer ~4 consensus waves per CU (wave census).
+    int *kslot = a.off_stbl >= 0 ? (int *)(smem + a.off_stbl) : nullptr;
+    uint32_t *stbl = a.off_stbl >= 0 ? (uint32_t *)(smem + a.off_stbl + 16) : nullptr;
+    if (kslot && threadIdx.x < 2) kslot[threadIdx.x] = 0;
+    if (wave < PPW) {
+        const int s0 = (int)blockIdx.x * PPW + wave;
+        RngPipe rp = pipe_of(wave);
+        // block 0 = the initial state (raw); flags
+        if (s0 < B.n_scans) {
+            if (B.mt_state_in) {
+                const uint32_t *src = B.mt_state_in + (size_t)s0 * 625;
+                for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
+            } else {
+                mt_seed(rp.blk, B.seeds ? B.seeds[s0] : 0u, lane);
+            }
+        }
+        if (lane < F_NFLAGS) rp.fl[lane] = 0;
+        if (s0 >= B.n_scans && lane == 0) rp.fl[F_BLKUSE] = -1;  // no scan: nothing to twist
+    }
+    __syncthreads();
+    if (kslot) {
+        const int s0 = (int)blockIdx.x * PPW + wave;
+        if (wave < PPW && s0 < B.n_scans && lane == 0 && a.rt_all) {
+            for (int c = B.scan_chunk_off[s0]; c < B.scan_chunk_off[s0 + 1]; c++) {
+                const int K = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c] - 1;
+                if (K < 2 || K > (int)RT_KMAX) continue;
+                const int o = atomicCAS(kslot, 0, K);
+                if (o == 0 || o == K) continue;
+                (void)atomicCAS(kslot + 1, 0, K);  // taken by another K: no table, mask mode
+            }
+        }
+        __syncthreads();
+        for (int t = 0; t < 2; t++) {
+            const int K = kslot[t];
+            if (K == 0) continue;
+            const uint32_t mK = 0xffffffffu >> __clz(K);
+            const uint4 *src = (const uint4 *)(a.rt_all + (size_t)(K - 2) * RT_DWORDS);
+            uint4 *dst = (uint4 *)(stbl + t * RT_DWORDS);
+            const uint32_t n4 = (mK + 1u) * RT_ST / 4u;
+            for (uint32_t e = threadIdx.x; e < n4; e += blockDim.x) dst[e] = src[e];
+        }
+        __syncthreads();
+    }
     if (wave < PPW) {
         const int s = (int)blockIdx.x * PPW + wave;
         RngPipe rp = pipe_of(wave);
@@ -1208,18 +1256,6 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         const uint64_t t_start = lslam_stamp();
         const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
-        // block 0 = the initial state (raw); flags
-        if (s < B.n_scans) {
-            if (B.mt_state_in) {
-                const uint32_t *src = B.mt_state_in + (size_t)s * 625;
-                for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
-            } else {
-                mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
-            }
-        }
-        if (lane < F_NFLAGS) rp.fl[lane] = 0;
-        if (s >= B.n_scans && lane == 0) rp.fl[F_BLKUSE] = -1;  // no scan: nothing to twist
-        __syncthreads();
         if (s >= B.n_scans) return;
         // ---- parser: its chain is the kernel's critical path
         const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
@@ -1240,10 +1276,19 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
             const int N = B.chunk_pt_off[c + 1] - p0;
             if (N < 3) continue;
             JT *Jc = J + (size_t)D * (size_t)p0;
-            if (a.rt_all && (uint32_t)N - 1u <= RT_KMAX) {
-                if (rp.tblK != (uint32_t)N - 1u) rt_load(rp, a.rt_all, (uint32_t)N - 1u, lane);
-                parse_chunk_tbl(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
-            } else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            bool tbl = a.rt_all && (uint32_t)N - 1u <= RT_KMAX;
+            if (tbl && kslot) {  // the workgroup's shared tables
+                const int K = N - 1;
+                tbl = kslot[0] == K || kslot[1] == K;
+                if (tbl) {
+                    rp.tbl = stbl + (kslot[0] == K ? 0 : RT_DWORDS);
+                    rp.tblK = (uint32_t)K;
+                }
+            } else if (tbl && rp.tblK != (uint32_t)N - 1u) {
+                rt_load(rp, a.rt_all, (uint32_t)N - 1u, lane);
+            }
+            if (tbl) parse_chunk_tbl(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
             else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
         }
         lds_flag_put(rp.fl + F_BLKUSE, -1);  // this pipe needs no more blocks
@@ -1274,7 +1319,7 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
 #endif
     } else {
         // ---- helper: twists on demand for every parser of the workgroup, asleep otherwise
-        __syncthreads();
+        // (block 0 and the flags are in: the workgroup barriers above)
         __builtin_amdgcn_s_setprio(3);
 #ifdef LSLAM_STAMPS
         if (a.dbg && lane == 0)
@@ -2889,9 +2934,15 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
     k.off_fl = off; off += align16(4 * F_NFLAGS);
     // the reject table: table mode is chosen per chunk (N - 1 <= RT_KMAX), so a batch whose
     // largest chunk is bigger may still parse its small chunks with it
-    k.off_tbl = off; off += k.rt_all ? align16(4 * RT_DWORDS) : 0;
+    static const bool shared = [] { const char *e = getenv("LSLAM_RT_SHARED"); return !(e && atoi(e) == 0); }();
+    k.off_stbl = -1;
+    k.off_tbl = off; off += (k.rt_all && !shared) ? align16(4 * RT_DWORDS) : 0;
     k.rng_pipe_bytes = off;
     lds = off * ppw;
+    if (k.rt_all && shared) {  // two K claims (16 B) + two tables, after the pipes
+        k.off_stbl = lds;
+        lds += 16 + 2 * 4 * RT_DWORDS;
+    }
     return LSLAM_OK;
 }
 
