@@ -138,6 +138,8 @@ struct KArgs {
     int ep_count;        // host: producer launches of the call
     size_t slot_jbytes;  // host: steps bytes of a slot (its MT state area follows)
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
+    const uint8_t *spec_dirty_in;  // fix-up: scans whose speculative producer input was stale (replay)
+    uint8_t *spec_dirty_out;       // fix-up: scans replayed by this call (the next call's dirty_in)
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     // large chunks (N > 128): count_kernel -> select_kernel
@@ -824,7 +826,12 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         // early-stopped chunk consumed a different stream; replay it whole
         bool any = false;
         for (int c = c0 + lane; c < c1; c += 64) any |= (B.models[c].flags & LSLAM_EARLY_STOP) != 0;
-        if (ballot(any) == 0ull) {
+        // a speculative producer (map mode) parsed this scan from the previous call's end state
+        // before that call's fix-up: if the fix-up replayed the scan, its draws are stale too
+        if (a.spec_dirty_in && lane == 0) any |= a.spec_dirty_in[s] != 0;
+        const bool replay = ballot(any) != 0ull;
+        if (a.spec_dirty_out && lane == 0) a.spec_dirty_out[s] = replay ? 1 : 0;
+        if (!replay) {
             // the producer's end state is the scan's
             if (B.mt_state_out && a.state_scr)
                 for (int i = lane; i < 625; i += 64)
@@ -1445,29 +1452,58 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
 // previous row, or the slot's front pad JBUF_FRONT) and walks only i <= K.
 constexpr int RR_GROUPS = 8;  // K <= 127
 constexpr size_t JBUF_FRONT = 64;  // bytes of a producer slot before its steps
-template <bool CHECK>
-__device__ __forceinline__ void rr_walk16(const uint4 v, uint32_t t, uint32_t K, uint32_t &c0, uint32_t &c1) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-        const uint32_t i = 16u * t + 1u + (uint32_t)u;  // byte 15 - u of the group
-        if (i < 2u) continue;                             // step 1: j_1 decides the final swap
-        if (CHECK && i > K) break;
-        const int off = 15 - u;
-        const uint32_t nb = 32u - (uint32_t)__clz((int)i);  // mask(i) = 2^nb - 1
-        const uint32_t j = __builtin_amdgcn_ubfe(w[off >> 2], (uint32_t)(8 * (off & 3)), nb);
-        c0 = (j == c0) ? i : c0;
-        c1 = (j == c1) ? i : c1;
+// One step of both trackers, c = (j == c) ? i : c.  The two trackers are independent
+// chains, so both compares are issued (masks in two SGPR pairs) before both selects; the
+// v_mov of i between them gives each select the two VALU wait states gfx950 requires
+// between a VALU write of a mask SGPR and v_cndmask reading it (the compiler's order --
+// compare, select, compare, select through VCC -- padded every step with s_nops: ~475 per
+// wave).  Only VALU instructions inside.
+template <uint32_t I>
+__device__ __forceinline__ void rr_step(uint32_t j, uint32_t &c0, uint32_t &c1) {
+    uint64_t m0, m1;
+    uint32_t iv;
+    asm volatile(
+        "v_cmp_eq_u32_e64 %[m0], %[j], %[c0]\n\t"
+        "v_cmp_eq_u32_e64 %[m1], %[j], %[c1]\n\t"
+        "v_mov_b32 %[iv], %[i]\n\t"
+        "v_cndmask_b32_e64 %[c0], %[c0], %[iv], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[c1], %[c1], %[iv], %[m1]"
+        : [c0] "+v"(c0), [c1] "+v"(c1), [m0] "=&s"(m0), [m1] "=&s"(m1), [iv] "=&v"(iv)
+        : [j] "v"(j), [i] "i"(I));
+}
+
+// steps i = 16T+1+U .. 16T+16 of a row's group T (byte 15 - U), all indices compile-time
+template <bool CHECK, uint32_t T, int U>
+__device__ __forceinline__ void rr_walk_from(const uint32_t (&w)[4], uint32_t K, uint32_t &c0, uint32_t &c1) {
+    if constexpr (U < 16) {
+        constexpr uint32_t i = 16u * T + 1u + (uint32_t)U;
+        if constexpr (i >= 2u) {  // step 1 (i = 1): j_1 decides the final swap, not a tracker step
+            if (CHECK && i > K) return;
+            constexpr int off = 15 - U;
+            constexpr uint32_t nb = 32u - (uint32_t)__builtin_clz(i);  // mask(i) = 2^nb - 1
+            const uint32_t j = __builtin_amdgcn_ubfe(w[off >> 2], (uint32_t)(8 * (off & 3)), nb);
+            rr_step<i>(j, c0, c1);
+        }
+        rr_walk_from<CHECK, T, U + 1>(w, K, c0, c1);
+    }
+}
+
+template <uint32_t T>
+__device__ __forceinline__ void rr_walk_groups(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t nfull, uint32_t &c0,
+                                               uint32_t &c1) {
+    if constexpr (T < (uint32_t)RR_GROUPS) {
+        const uint32_t ws[4] = {w[T].x, w[T].y, w[T].z, w[T].w};
+        if (T < nfull) {
+            rr_walk_from<false, T, 0>(ws, K, c0, c1);
+            rr_walk_groups<T + 1>(w, K, nfull, c0, c1);
+        } else if (T == nfull) {
+            rr_walk_from<true, T, 0>(ws, K, c0, c1);
+        }
     }
 }
 
 __device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t &c0, uint32_t &c1) {
-    const uint32_t nfull = K >> 4;  // groups with all 16 steps <= K
-#pragma unroll
-    for (int t = 0; t < RR_GROUPS; t++) {
-        if ((uint32_t)t < nfull) rr_walk16<false>(w[t], (uint32_t)t, K, c0, c1);
-        else if ((uint32_t)t == nfull) rr_walk16<true>(w[t], (uint32_t)t, K, c0, c1);
-    }
+    rr_walk_groups<0>(w, K, K >> 4, c0, c1);  // K >> 4 groups with all 16 steps <= K
 }
 
 __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
@@ -2252,6 +2288,16 @@ struct lslam_ctx {
     const void *prev_state_out;
     int prev_slot;
     int prev_fixed;
+    // speculative producer (map mode): a call whose only producer hazard is the previous call's
+    // mt_state_out parses from the previous producer's end state (its slot's state area) without
+    // waiting for that call's fix-up; the fix-up replays the scans it replayed (spec_dirty)
+    int speculate;            // env LSLAM_MT_SPECULATE=0: wait for the fix-up (A/B)
+    int spec_ok;              // the previous call was a one-epoch pipeline call with dirty flags
+    const uint32_t *prev_state_scr;
+    int prev_spec_scans;
+    uint8_t *spec_dirty[2];   // [n_scans] replayed-by-fix-up flags, by call parity
+    int spec_dirty_n;
+    int spec_cur;             // the buffer the latest fix-up wrote
 };
 
 static thread_local std::string g_err;
@@ -2379,6 +2425,14 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->pslot[0] = c->pslot[1] = nullptr;
     c->pslot_bytes = 0;
     c->next_slot = 0;
+    c->speculate = 1;
+    if (const char *e = getenv("LSLAM_MT_SPECULATE")) c->speculate = atoi(e) != 0;
+    c->spec_ok = 0;
+    c->prev_state_scr = nullptr;
+    c->prev_spec_scans = 0;
+    c->spec_dirty[0] = c->spec_dirty[1] = nullptr;
+    c->spec_dirty_n = 0;
+    c->spec_cur = 0;
     c->n_out = 0;
     for (int k = 0; k < LSLAM_K_COUNT; k++) {
         c->total_ms[k] = 0;
@@ -2445,6 +2499,8 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     for (int i = 0; i < 2; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
     if (c->rt_all) (void)hipFree(c->rt_all);
+    for (int i = 0; i < 2; i++)
+        if (c->spec_dirty[i]) (void)hipFree(c->spec_dirty[i]);
     hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
@@ -3013,6 +3069,7 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
             HIPCHK(e);
         }
         c->pslot_bytes = jbytes + sbytes;
+        c->spec_ok = 0;  // the previous producer's end state went with the old slots
     }
     k.jbuf = (unsigned char *)c->pslot[slot] + JBUF_FRONT;
     k.state_scr = (uint32_t *)((unsigned char *)c->pslot[slot] + jbytes);
@@ -3374,6 +3431,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     int st = build_args(k, b, p, nullptr, MODE_RANSAC, lds_fix);
     if (st) return st;
     const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
+    bool spec = false;
     int slot = c->next_slot;
     if (mt) {
         st = prepare_steps(c, k, slot);
@@ -3443,13 +3501,21 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
             c->n_out = 0;
             c->out_unknown = 0;
         }
-        if (hz == 1) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
-        // a producer that waited on the previous call (a chained stream: LandmarkMap steps) will
-        // most likely wait on this one too, so this call's resolve runs alone: the LDS-staged
-        // form is faster there (map mode 1.48 vs 1.39 ms per step); otherwise the next call's
-        // producer runs beside it and holds the LDS (C3 0.93 vs 1.03 ms)
-        c->resolve_beside = hz == 0;
+        // speculation (a chained stream, e.g. LandmarkMap steps): parse from the previous
+        // producer's end state, which precedes this producer on pstream, instead of waiting for
+        // the previous fix-up; this call's fix-up replays the scans that one replayed
+        spec = hz == 1 && c->speculate && c->spec_ok && k.ep_count == 1 && c->prev_state_scr &&
+               c->prev_spec_scans == b->n_scans && b->mt_state_in == c->prev_state_out;
+        if (hz == 1 && !spec) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
+        // a producer that waited on the previous call will most likely wait on this one too, so
+        // this call's resolve runs alone: the LDS-staged form is faster there (map mode 1.48 vs
+        // 1.39 ms per step); otherwise the next call's producer runs beside it and holds the LDS
+        // (C3 0.93 vs 1.03 ms)
+        c->resolve_beside = hz == 0 || spec;
+        const uint32_t *true_in = k.b.mt_state_in;
+        if (spec) k.b.mt_state_in = c->prev_state_scr;
         st = produce_draws(c, k, slot, c->pstream, nullptr, slot);  // slot <- the last epoch's
+        k.b.mt_state_in = true_in;  // the fix-up's replays start from the true state
         if (st) return st;
     }
     // a UKF that reads nothing of this call's RANSAC may run anywhere in the ctx chain
@@ -3470,6 +3536,27 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (mt) {
         KArgs kf = k;
         kf.fixup = 1;
+        // replay flags: this call's, for the next call's speculation (one epoch only: the
+        // end state is then the slot's state area)
+        if (k.ep_count == 1 && b->mt_state_out) {
+            if (c->spec_dirty_n < b->n_scans) {
+                HIPCHK(hipStreamSynchronize(c->stream));
+                for (int i = 0; i < 2; i++) {
+                    if (c->spec_dirty[i]) HIPCHK(hipFree(c->spec_dirty[i]));
+                    c->spec_dirty[i] = nullptr;
+                }
+                c->spec_dirty_n = 0;
+                for (int i = 0; i < 2; i++) {
+                    hipError_t e = hipMalloc(&c->spec_dirty[i], (size_t)b->n_scans);
+                    if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (flags)");
+                    HIPCHK(e);
+                }
+                c->spec_dirty_n = b->n_scans;
+                if (spec) return set_err(LSLAM_ERR_HIP, "speculation without replay flags");  // unreachable
+            }
+            kf.spec_dirty_in = spec ? c->spec_dirty[c->spec_cur] : nullptr;
+            kf.spec_dirty_out = c->spec_dirty[c->spec_cur ^ 1];
+        }
         static std::once_flag once;
         std::call_once(once, [] { set_max_lds(scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>); });
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_fix,
@@ -3481,6 +3568,12 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     c->prev_state_out = mt ? b->mt_state_out : nullptr;
     c->prev_slot = slot;
     c->prev_fixed = mt ? 1 : 0;
+    c->spec_ok = (mt && k.ep_count == 1 && b->mt_state_out) ? 1 : 0;
+    if (c->spec_ok) {
+        c->spec_cur ^= 1;  // the buffer this call's fix-up writes
+        c->prev_state_scr = k.state_scr;
+        c->prev_spec_scans = b->n_scans;
+    }
     switch (pmode) {
         case MODE_ASSOC | MODE_UKF: st = launch_post<MODE_ASSOC | MODE_UKF>(c, kp, lds_post); break;
         case MODE_POST | MODE_UKF: st = launch_post<MODE_POST | MODE_UKF>(c, kp, lds_post); break;
@@ -3586,6 +3679,7 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     c->prev_state_out = b->mt_state_out;
     c->prev_slot = last;
     c->prev_fixed = b->mt_state_out ? 1 : 0;
+    c->spec_ok = 0;
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_HYP);
 }
