@@ -119,6 +119,7 @@ class DeviceArray:
             raise ValueError("upload size mismatch %d != %d" % (arr.nbytes, self.nbytes))
         _lib.check(self.ctx._L.lslam_h2d(self.ctx.handle, self.ptr, arr.ctypes.data_as(C.c_void_p),
                                          self.nbytes), "lslam_h2d")
+        self.ctx._inflight.append(arr)  # held until the next sync(), whoever else drops it
 
     def download_async(self, out):
         """D2H on the context stream without waiting: ``out`` (a C-contiguous host array of

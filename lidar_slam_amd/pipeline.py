@@ -179,6 +179,8 @@ class ScanPipeline:
                 self.inputs.get(k)
             if dst is None:
                 raise KeyError("no device input %r" % k)
+            # a converted copy is a temporary: DeviceArray.upload_async parks it on
+            # ctx._inflight until the next sync, so the copy never reads freed memory
             dst.upload_async(np.ascontiguousarray(v, dst.dtype).reshape(dst.shape))
 
     def clear_lists_async(self):
