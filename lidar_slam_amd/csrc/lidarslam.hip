@@ -116,6 +116,7 @@ struct KArgs {
     int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum, off_inl;
     int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg, off_zobs;
     int corg_cap;
+    int off_recs;       // post pass: the scan's chunk records + chunk offsets (-1: per-chunk loop)
     int off_ukf;
     int off_j1;
     int pts_cap;
@@ -791,6 +792,87 @@ __device__ __forceinline__ double2 observe_point(const lslam_chunk_model &r, dou
 }
 
 // ------------------------------------------------------------------------
+// A9/A10 post pass over fitted models (ransac_functions.py:34-55, landmarking.py:48-77),
+// not MAP mode.  The per-chunk loop of scan_body makes ~3 dependent HBM round trips per
+// chunk (its record, its mask, its x); a post wave is one scan's serial chain, and beside
+// the next call's producer (5 of a SIMD's 8 wave slots) a 4096-scan batch needs two rounds
+// of post waves, so those round trips set the kernel's time.  Here the scan's records and
+// chunk offsets come in with one 16-byte load per lane, the walk runs on LDS only, and the
+// records and y_proj go out in flat passes (4 points per lane in flight).  Same values,
+// same order of list updates as the loop.
+// ------------------------------------------------------------------------
+__device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int id0, lslam_landmark *lmk,
+                                uint64_t *vis, int &L, double2 *corg, unsigned char *rbuf, int lane) {
+    static_assert(sizeof(lslam_chunk_model) == 112, "a chunk record is 7 x 16 bytes");
+    const lslam_scan_batch &B = a.b;
+    lslam_chunk_model *recs = (lslam_chunk_model *)rbuf;
+    int32_t *off = (int32_t *)(rbuf + (((int)sizeof(lslam_chunk_model) * a.hist_cap + 15) & ~15));  // hist_cap = max_scan_chunks
+    {
+        const uint4 *src = (const uint4 *)(B.models + c0);
+        uint4 *dst = (uint4 *)rbuf;
+        for (int e = lane; e < nchunks * 7; e += 64) dst[e] = src[e];
+        for (int e = lane; e <= nchunks; e += 64) off[e] = B.chunk_pt_off[c0 + e];
+    }
+    __syncthreads();
+    int32_t *walk = B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr;
+    for (int ci = 0; ci < nchunks; ci++) {
+        lslam_chunk_model rec = recs[ci];
+        rec.landmark_id = id0 + ci;
+        const bool have_model = (rec.flags & LSLAM_VALID) != 0;
+        if (ci < a.corg_cap && lane == 0)
+            corg[ci] = have_model ? make_double2(rec.ox, rec.oy) : make_double2(__builtin_nan(""), __builtin_nan(""));
+        if (have_model) {
+            double pa, pb;
+            bool overflow = false;
+            const int m = associate(a, lmk, vis, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
+                                    rec.landmark_id, pa, pb, overflow, walk, lane);
+            rec.match_index = m;
+            rec.proj_a = pa;
+            rec.proj_b = pb;
+            rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
+            if (overflow) rec.flags |= LSLAM_CAPACITY;
+        }
+        __syncthreads();  // every lane has its copy of recs[ci]
+        if (lane == 0) recs[ci] = rec;
+    }
+    __syncthreads();
+    {
+        const uint4 *src = (const uint4 *)rbuf;
+        uint4 *dst = (uint4 *)(B.models + c0);
+        for (int e = lane; e < nchunks * 7; e += 64) dst[e] = src[e];
+    }
+    if (!B.y_proj) return;
+    // y_proj: point q of chunk ci (off[ci] <= q < off[ci + 1]); a lane's points ascend, so
+    // its chunk index only moves forward
+    const int q0 = off[0], q1 = off[nchunks];
+    int ci = 0;
+    for (int qb = q0; qb < q1; qb += 4 * 64) {
+        uint8_t mk[4];
+        double xs[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = qb + u * 64 + lane;
+            mk[u] = 0;
+            xs[u] = 0.0;
+            if (q < q1) {
+                mk[u] = B.inlier_mask[q];
+                xs[u] = B.xy ? B.xy[2 * (size_t)q] : polar_xy(B.theta_deg[q], B.dist_mm[q]).x;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = qb + u * 64 + lane;
+            if (q < q1) {
+                while (ci + 1 < nchunks && off[ci + 1] <= q) ci++;
+                const lslam_chunk_model &r = recs[ci];
+                const bool have_model = (r.flags & LSLAM_VALID) != 0;
+                B.y_proj[q] = (have_model && mk[u]) ? (r.proj_a * xs[u] + r.proj_b) : 0.0;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
 // the scan kernel
 // ------------------------------------------------------------------------
 template <int HYP, int MODE>
@@ -898,7 +980,14 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
         sth = sin(mx[2]);
     }
 
-    for (int ci = 0; ci < nchunks && (kRansac || kPost); ci++) {
+    bool chunks_done = false;
+    if constexpr (kPost && (MODE & MODE_ASSOC) != 0) {
+        if (!map_mode && a.off_recs >= 0) {
+            post_assoc_fast(a, s, c0, nchunks, id0, lmk, vis, L, corg, smem + a.off_recs, lane);
+            chunks_done = true;
+        }
+    }
+    for (int ci = 0; ci < nchunks && (kRansac || kPost) && !chunks_done; ci++) {
         const int c = c0 + ci;
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
@@ -2866,9 +2955,18 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         k.off_mask = off; off += align16(N);
         k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
         k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
+        k.off_recs = -1;
     } else {
         // post pass (association / UKF over fitted models): only the chunk's mask
         k.off_mask = off; off += align16(N);
+        // and the scan's chunk records + offsets, staged up front (post_assoc_fast)
+        const int msc = b->max_scan_chunks > 0 ? b->max_scan_chunks : 1;
+        if (msc <= 256) {
+            k.off_recs = off;
+            off += align16((int)sizeof(lslam_chunk_model) * msc) + align16(4 * (msc + 1));
+        } else {
+            k.off_recs = -1;
+        }
     }
     // the UKF runs after the last chunk: its scratch aliases the RANSAC scratch
     // above (offset 0); only the persistent region below (chunk history, chunk
@@ -3519,8 +3617,12 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         if (st) return st;
     }
     // a UKF that reads nothing of this call's RANSAC may run anywhere in the ctx chain
-    // (LSLAM_UKF_EARLY: 0 after the post pass, 1 before the fix-up, 2 before the consensus)
-    static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 0; }();
+    // (LSLAM_UKF_EARLY: 0 after the post pass, 1 before the fix-up, 2 before the consensus,
+    // 3 = default: between the fix-up and the post pass).  The fix-up releases this call's
+    // steps slot; the next producer starts ~40 us after that event, so a UKF placed right
+    // behind the fix-up runs alone (35 us) instead of beside the parsers (~180 us): C3
+    // 0.893 -> 0.858 ms per step, the producer 0.79 -> 0.71 ms in the pipeline
+    static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 3; }();
     const bool ukf_indep = ukf_lane && !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
     const int ukf_at = ukf_indep ? ukf_early : 0;
     if (ukf_lane && ukf_at == 2) {
@@ -3563,6 +3665,10 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
                            c->stream, kf);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+    }
+    if (ukf_lane && ukf_at == 3) {
+        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
+        HIPCHK(hipGetLastError());
     }
     // (mt_state_out is final after the fix-up: the next call's producer may chain from it early)
     c->prev_state_out = mt ? b->mt_state_out : nullptr;

@@ -34,7 +34,7 @@ def counter(path, name, kernel_sub="scan_kernel"):
 
 
 # kernel-name substrings: producer, consensus, fix-up (scan_kernel<MT, RANSAC>), post pass (scan_kernel<EXPLICIT, ...>)
-KERNELS = {"rng_kernel": "rng_kernel", "resolve_reg_kernel": "resolve_reg_kernel", "resolve_kernel": "resolve_kernel<",
+KERNELS = {"rng_kernel": "rng_kernel", "resolve_reg": "resolve_reg", "resolve_kernel": "resolve_kernel<",
            "chunk_kernel": "chunk_kernel", "ukf_group_kernel": "ukf_group_kernel", "fixup": "scan_kernel<0, 1>",
            "post": "scan_kernel<2, "}
 
@@ -81,8 +81,8 @@ def main(tag, bench_log=None):
                      % (k, v["fetch_kib"], v["write_kib"], v["bytes_per_launch"]))
     cfg = bench["config"]
     st, dr = resolve_alg_bytes(cfg["points_per_scan"], cfg["scans_per_gpu"], cfg["trials"])
-    if "resolve_reg_kernel" in per:
-        v = per["resolve_reg_kernel"]
+    if "resolve_reg" in per:  # resolve_reg_kernel or resolve_reg8_kernel
+        v = per["resolve_reg"]
         lines += ["", "Resolve, algorithmic vs PMC: steps read %d B + draws written %d B = %d B per launch; PMC read "
                   "%d B (x2 corrected), written %d B." % (st, dr, st + dr, int(2 * v["fetch_kib"] * 1024),
                                                          int(v["write_kib"] * 1024))]
