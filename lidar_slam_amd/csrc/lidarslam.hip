@@ -668,7 +668,19 @@ __device__ __forceinline__ bool is_equal(const lslam_landmark &Lk, double a, dou
 // returns match index (pre-call) or -1; updates list + count; proj line out
 __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, int &L, double a, double b,
                          double px, double py, double ex, double ey, int id, double &pa, double &pb,
-                         bool &overflow, int32_t *walk_out, int lane, double2 *mpos = nullptr) {
+                         bool &overflow, int32_t *walk_out, int lane, double2 *mpos = nullptr,
+                         unsigned long long *st = nullptr) {
+#ifdef LSLAM_STAMPS
+    uint64_t _as_prev = lslam_stamp();
+#define AS_STAMP(k)                                                    \
+    do {                                                               \
+        const uint64_t _t = lslam_stamp();                             \
+        if (st && lane == 0) st[(k)] += _t - _as_prev;                 \
+        _as_prev = _t;                                                 \
+    } while (0)
+#else
+#define AS_STAMP(k) do {} while (0)
+#endif
     const int nblk = (L + 63) >> 6;
     for (int i = lane; i < nblk; i += 64) vis[i] = 0ull;
     __syncthreads();
@@ -687,20 +699,40 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
         }
         const uint64_t E = ballot(eq);
         const uint64_t D = ballot(dies);
-        uint64_t V = 0;
-        const int hi = min(L, blk * 64 + 64);
-        while (k < hi) {
-            const int bit = k - blk * 64;
-            if ((E >> bit) & 1ull) {
-                match = k;
-                break;
-            }
-            V |= 1ull << bit;
-            k += ((D >> bit) & 1ull) ? 2 : 1;
+        AS_STAMP(12);
+        // The walk as bit operations on the two ballots (a serial loop here was SALU and
+        // branch bound: ~half the post pass beside the producer, whose parsers keep the CU's
+        // scalar unit busy).  Position p is visited unless p-1 was visited and died (its
+        // removal makes `i += 1` skip p): in a run of dying entries [r, e] that starts at a
+        // visited position, r, r+2, r+4, ... are visited and r+1, r+3, ... (up to e+1) skipped.
+        // Adding a run's start bit carries through the run, so Dm & ~(Dm + starts) selects the
+        // runs by the parity of their start.  tests/test_assoc_walk_bits.py checks this form
+        // against the serial walk on random lists of 1..200 entries.
+        const int base = blk * 64;
+        const int s0 = k - base;                   // 0, or 1 after a skip across the block end
+        const int n = min(L, base + 64) - base;    // list positions in this block
+        const uint64_t valid = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+        const uint64_t ge = ~0ull << s0;
+        const uint64_t Dm = D & valid & ge;
+        const uint64_t run0 = Dm & ~(Dm << 1);     // first entry of each run of dying entries
+        const uint64_t EVEN = 0x5555555555555555ull;
+        const uint64_t Re = Dm & ~(Dm + (run0 & EVEN));        // runs starting at an even position
+        const uint64_t EO = (Re & EVEN) | (Dm & ~Re & ~EVEN);  // even offset within their run
+        const uint64_t visited = ge & valid & ~(EO << 1);
+        const uint64_t hits = visited & E;
+        uint64_t V;
+        if (hits) {
+            const int m = ffs64(hits);
+            match = base + m;
+            V = visited & ((1ull << m) - 1ull);
+        } else {
+            V = visited;
+            k = n >= 64 ? base + 64 + (int)(EO >> 63) : base + n;
         }
         if (lane == 0) vis[blk] = V;
         __syncthreads();
     }
+    AS_STAMP(9);
     pa = a;
     pb = b;
     if (match >= 0) {
@@ -733,6 +765,7 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
         __syncthreads();
     }
     L = w;
+    AS_STAMP(10);
     overflow = false;
     if (match < 0) {
         if (L < ka.lmk_cap) {
@@ -748,6 +781,7 @@ __device__ int associate(const KArgs &ka, lslam_landmark *lmk, uint64_t *vis, in
         }
     }
     __syncthreads();
+    AS_STAMP(11);
     return match;
 }
 
@@ -801,9 +835,23 @@ __device__ __forceinline__ double2 observe_point(const lslam_chunk_model &r, dou
 // records and y_proj go out in flat passes (4 points per lane in flight).  Same values,
 // same order of list updates as the loop.
 // ------------------------------------------------------------------------
+// diagnostic build only: post-pass phase cycles into dbg[(n_chunks + s) * 16 + k]
+#ifdef LSLAM_STAMPS
+#define PS_STAMP(k)                                                                               \
+    do {                                                                                          \
+        const uint64_t _t = lslam_stamp();                                                        \
+        if (a.dbg && lane == 0) a.dbg[((size_t)a.b.n_chunks + s) * 16 + (k)] += _t - _ps_prev;  \
+        _ps_prev = _t;                                                                            \
+    } while (0)
+#define PS_STAMP_DECL uint64_t _ps_prev = lslam_stamp();
+#else
+#define PS_STAMP(k) do {} while (0)
+#define PS_STAMP_DECL
+#endif
 __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int id0, lslam_landmark *lmk,
                                 uint64_t *vis, int &L, double2 *corg, unsigned char *rbuf, int lane) {
     static_assert(sizeof(lslam_chunk_model) == 112, "a chunk record is 7 x 16 bytes");
+    PS_STAMP_DECL
     const lslam_scan_batch &B = a.b;
     lslam_chunk_model *recs = (lslam_chunk_model *)rbuf;
     int32_t *off = (int32_t *)(rbuf + (((int)sizeof(lslam_chunk_model) * a.hist_cap + 15) & ~15));  // hist_cap = max_scan_chunks
@@ -814,6 +862,7 @@ __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int 
         for (int e = lane; e <= nchunks; e += 64) off[e] = B.chunk_pt_off[c0 + e];
     }
     __syncthreads();
+    PS_STAMP(1);
     int32_t *walk = B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr;
     for (int ci = 0; ci < nchunks; ci++) {
         lslam_chunk_model rec = recs[ci];
@@ -824,8 +873,13 @@ __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int 
         if (have_model) {
             double pa, pb;
             bool overflow = false;
+#ifdef LSLAM_STAMPS
+            unsigned long long *st = a.dbg ? a.dbg + ((size_t)a.b.n_chunks + s) * 16 : nullptr;
+#else
+            unsigned long long *st = nullptr;
+#endif
             const int m = associate(a, lmk, vis, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
-                                    rec.landmark_id, pa, pb, overflow, walk, lane);
+                                    rec.landmark_id, pa, pb, overflow, walk, lane, nullptr, st);
             rec.match_index = m;
             rec.proj_a = pa;
             rec.proj_b = pb;
@@ -836,11 +890,13 @@ __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int 
         if (lane == 0) recs[ci] = rec;
     }
     __syncthreads();
+    PS_STAMP(2);
     {
         const uint4 *src = (const uint4 *)rbuf;
         uint4 *dst = (uint4 *)(B.models + c0);
         for (int e = lane; e < nchunks * 7; e += 64) dst[e] = src[e];
     }
+    PS_STAMP(3);
     if (!B.y_proj) return;
     // y_proj: point q of chunk ci (off[ci] <= q < off[ci + 1]); a lane's points ascend, so
     // its chunk index only moves forward
@@ -870,6 +926,7 @@ __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int 
             }
         }
     }
+    PS_STAMP(4);
 }
 
 // ------------------------------------------------------------------------
@@ -1208,8 +1265,17 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
     WAVE_CENSUS(a, a.fixup ? WC_FIXUP : WC_POST);
     if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);
     for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
+#ifdef LSLAM_STAMPS
+        const uint64_t t0 = lslam_stamp();
+#endif
         scan_body<HYP, MODE>(a, s, smem);
         __syncthreads();
+#ifdef LSLAM_STAMPS
+        if (!a.fixup && a.dbg && threadIdx.x == 0) {
+            a.dbg[((size_t)a.b.n_chunks + s) * 16 + 7] += lslam_stamp() - t0;
+            a.dbg[((size_t)a.b.n_chunks + s) * 16 + 8] = t0;
+        }
+#endif
     }
 }
 template <int HYP, int MODE>
