@@ -1449,7 +1449,8 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
             } else if (tbl && rp.tblK != (uint32_t)N - 1u) {
                 rt_load(rp, a.rt_all, (uint32_t)N - 1u, lane);
             }
-            if (tbl) parse_chunk_tbl(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            if (tbl && N - 1 >= 64) parse_chunk_tbl<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+            else if (tbl) parse_chunk_tbl<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
             else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
             else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
         }
@@ -1659,6 +1660,112 @@ __device__ __forceinline__ void rr_walk_groups(const uint4 (&w)[RR_GROUPS], uint
 
 __device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t &c0, uint32_t &c1) {
     rr_walk_groups<0>(w, K, K >> 4, c0, c1);  // K >> 4 groups with all 16 steps <= K
+}
+
+// Two groups of 64 draws per wave (lane l walks draws d and d + 64 of its chunk at once):
+// the two walks are independent chains, interleaved step by step (four compares, then four
+// selects), so a wave keeps twice the work in flight.  Beside the producer a SIMD holds ~3
+// consumer waves and the walk is a dependent compare -> select chain per step: C3's 101 draws
+// per chunk were two waves of which the second had 37 live lanes.
+template <uint32_t I>
+__device__ __forceinline__ void rr_step2(uint32_t ja, uint32_t jb, uint32_t &a0, uint32_t &a1, uint32_t &b0,
+                                         uint32_t &b1) {
+    uint64_t m0, m1, m2, m3;
+    uint32_t iv;
+    asm volatile(
+        "v_cmp_eq_u32_e64 %[m0], %[ja], %[a0]\n\t"
+        "v_cmp_eq_u32_e64 %[m1], %[ja], %[a1]\n\t"
+        "v_cmp_eq_u32_e64 %[m2], %[jb], %[b0]\n\t"
+        "v_cmp_eq_u32_e64 %[m3], %[jb], %[b1]\n\t"
+        "v_mov_b32 %[iv], %[i]\n\t"
+        "v_cndmask_b32_e64 %[a0], %[a0], %[iv], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[a1], %[a1], %[iv], %[m1]\n\t"
+        "v_cndmask_b32_e64 %[b0], %[b0], %[iv], %[m2]\n\t"
+        "v_cndmask_b32_e64 %[b1], %[b1], %[iv], %[m3]"
+        : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1), [m0] "=&s"(m0), [m1] "=&s"(m1),
+          [m2] "=&s"(m2), [m3] "=&s"(m3), [iv] "=&v"(iv)
+        : [ja] "v"(ja), [jb] "v"(jb), [i] "i"(I));
+}
+
+template <bool CHECK, uint32_t T, int U>
+__device__ __forceinline__ void rr_walk_from2(const uint32_t (&wa)[4], const uint32_t (&wb)[4], uint32_t K,
+                                              uint32_t &a0, uint32_t &a1, uint32_t &b0, uint32_t &b1) {
+    if constexpr (U < 16) {
+        constexpr uint32_t i = 16u * T + 1u + (uint32_t)U;
+        if constexpr (i >= 2u) {
+            if (CHECK && i > K) return;
+            constexpr int off = 15 - U;
+            constexpr uint32_t nb = 32u - (uint32_t)__builtin_clz(i);
+            const uint32_t ja = __builtin_amdgcn_ubfe(wa[off >> 2], (uint32_t)(8 * (off & 3)), nb);
+            const uint32_t jb = __builtin_amdgcn_ubfe(wb[off >> 2], (uint32_t)(8 * (off & 3)), nb);
+            rr_step2<i>(ja, jb, a0, a1, b0, b1);
+        }
+        rr_walk_from2<CHECK, T, U + 1>(wa, wb, K, a0, a1, b0, b1);
+    }
+}
+
+template <uint32_t T>
+__device__ __forceinline__ void rr_walk_groups2(const uint4 (&wa)[RR_GROUPS], const uint4 (&wb)[RR_GROUPS], uint32_t K,
+                                                uint32_t nfull, uint32_t &a0, uint32_t &a1, uint32_t &b0,
+                                                uint32_t &b1) {
+    if constexpr (T < (uint32_t)RR_GROUPS) {
+        const uint32_t xa[4] = {wa[T].x, wa[T].y, wa[T].z, wa[T].w};
+        const uint32_t xb[4] = {wb[T].x, wb[T].y, wb[T].z, wb[T].w};
+        if (T < nfull) {
+            rr_walk_from2<false, T, 0>(xa, xb, K, a0, a1, b0, b1);
+            rr_walk_groups2<T + 1>(wa, wb, K, nfull, a0, a1, b0, b1);
+        } else if (T == nfull) {
+            rr_walk_from2<true, T, 0>(xa, xb, K, a0, a1, b0, b1);
+        }
+    }
+}
+
+__device__ __forceinline__ void rr_store(const KArgs &a, int c, uint32_t d, uint32_t j1w, uint32_t c0, uint32_t c1) {
+    const uint32_t Dall = (uint32_t)a.T + 1u;
+    const uint32_t j1 = (j1w >> 24) & 1u;  // byte K - 1: step 1
+    int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)(a.ep_d0 + d);
+    draws[0] = (int32_t)((j1 == 0u) ? c1 : c0);
+    draws[1] = (int32_t)((j1 == 0u) ? c0 : c1);
+}
+
+__global__ __launch_bounds__(64) void resolve_reg8x2_kernel(const KArgs a) {
+    const int lane = (int)threadIdx.x;
+    const lslam_scan_batch &B = a.b;
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : (uint32_t)a.T + 1u;
+    const int np = (int)((D + 127u) >> 7);  // waves per chunk: lanes x 2 = 128 draws
+    WAVE_CENSUS(a, WC_RESOLVE);
+    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
+    const int64_t total = (int64_t)B.n_chunks * np;
+    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
+        const int c = (int)(e / np);
+        const uint32_t d0 = 128u * (uint32_t)(e - (int64_t)c * np);
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        const uint32_t K = (uint32_t)N - 1u;  // <= 127 (host)
+        const uint8_t *J = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0;
+        const uint32_t da = d0 + (uint32_t)lane, db = da + 64u;
+        const uint8_t *ra = J + (size_t)(da < D ? da : 0u) * K;
+        uint4 wa[RR_GROUPS];
+#pragma unroll
+        for (int t = 0; t < RR_GROUPS; t++)
+            if ((uint32_t)(16 * t) < K) wa[t] = load16_unaligned(ra + (int)K - 16 * (t + 1));
+        if (d0 + 64u < D) {  // wave-uniform: the second group has live draws
+            const uint8_t *rb = J + (size_t)(db < D ? db : 0u) * K;
+            uint4 wb[RR_GROUPS];
+#pragma unroll
+            for (int t = 0; t < RR_GROUPS; t++)
+                if ((uint32_t)(16 * t) < K) wb[t] = load16_unaligned(rb + (int)K - 16 * (t + 1));
+            uint32_t a0 = 0, a1 = 1, b0 = 0, b1 = 1;
+            rr_walk_groups2<0>(wa, wb, K, K >> 4, a0, a1, b0, b1);
+            if (da < D) rr_store(a, c, da, wa[0].w, a0, a1);
+            if (db < D) rr_store(a, c, db, wb[0].w, b0, b1);
+        } else {
+            uint32_t a0 = 0, a1 = 1;
+            rr_walk_row(wa, K, a0, a1);
+            if (da < D) rr_store(a, c, da, wa[0].w, a0, a1);
+        }
+    }
 }
 
 __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
@@ -2563,7 +2670,8 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     }
     {
         const char *e = getenv("LSLAM_RESOLVE_REG");
-        c->resolve_reg = e ? (atoi(e) == 2 ? 2 : atoi(e) == 0 ? 0 : 1) : 1;  // 2: the 16-step walk (A/B)
+        // 2: the 16-step walk, 3: two groups of 64 draws per wave (A/B)
+        c->resolve_reg = e ? (atoi(e) == 3 ? 3 : atoi(e) == 2 ? 2 : atoi(e) == 0 ? 0 : 1) : 1;
     }
     c->resolve_beside = 0;
     c->timing_mask = 0xffffffffu;
@@ -3281,7 +3389,10 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         return LSLAM_OK;
     }
     if (k.j8 && c->resolve_reg && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
-        if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg != 2) {
+        if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg == 3) {
+            const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 127) / 128))), block(64);
+            hipLaunchKernelGGL(resolve_reg8x2_kernel, grid, block, 0, c->stream, k);
+        } else if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg != 2) {
             const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 63) / 64))), block(64);
             hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, c->stream, k);
         } else {

@@ -339,9 +339,11 @@ __device__ __forceinline__ uint32_t step_mask(uint32_t i) { return 0xffffffffu >
 __device__ __forceinline__ bool rt_rej(uint64_t M, uint32_t s) { return (int32_t)(uint32_t)((M << s) >> 32) < 0; }
 
 // (sg + na) mod K for sg < K, na <= 64: one conditional subtraction when K >= 64
+// (KGE64, known at compile time: no per-window test of K)
+template <bool KGE64>
 __device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
     x = min(x, x - K);  // unsigned: x - K wraps high when x < K
-    if (K < 64)
+    if (!KGE64)
         while (x >= K) x -= K;
     return x;
 }
@@ -354,8 +356,12 @@ __device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
     return (y ^ (y >> 18)) & mK;
 }
 
+typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
 __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
-    const uint32_t *row = tbl + v * RT_ST + (sg >> 5);
+    // 32-bit LDS byte address: v * 28 (v <= 127) as one u24 multiply-add onto the scalar
+    // part (table base + dword sg / 32), not a 64-bit generic-pointer multiply-add
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32_t *)tbl + ((sg >> 5) << 2);
+    lds_u32_t *row = (lds_u32_t *)(uintptr_t)(__umul24(v, RT_ST * 4u) + base);
     const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
     const uint32_t r = sg & 31u;
     const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, r);
@@ -374,7 +380,47 @@ __device__ __forceinline__ void rt_load(RngPipe &rp, const uint32_t *__restrict_
     rp.tblK = K;
 }
 
-template <typename JT>
+// One full table-mode window (64 words, short of the chunk's end).  Only the last window of a
+// run may run across the block's end (CHECK): the others skip that test, so the run loop
+// carries one backward branch per window.
+template <bool CHECK, bool KGE64, typename JT>
+__device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int blkno, int &pos, uint32_t &raw,
+                                           uint32_t &g, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
+                                           uint32_t sbase, uint32_t s0, int lane) {
+    if (CHECK && pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
+        while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        raw = kb[pos + lane];
+    }
+    // next window's words (after a crossing window: discarded by the block switch)
+    const uint32_t nraw = kb[pos + 64 + lane];
+    const uint32_t v = rt_temper_mask(raw, mK);
+    const uint64_t M = rt_window(rp.tbl, v, sg);
+    // three evaluations without a convergence check (one more evaluation of the fixed point
+    // leaves it unchanged; ~5 are needed on average), then one per check: fewer VALU -> SALU
+    // round trips and branches
+    uint64_t R = ballot(rt_rej(M, s0));
+#pragma unroll
+    for (int e = 0; e < 3; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
+    uint32_t s;
+    RP_COUNT(6, 4);
+    for (;;) {
+        s = mbcnt_from(R, sbase);
+        const uint64_t Rn = ballot(rt_rej(M, s));
+        RP_COUNT(6, 1);
+        if (Rn == R) break;
+        R = Rn;
+    }
+    RP_COUNT(5, 1);
+    store_accepted(J, (g + 63u) - s, v, R);
+    const uint32_t na = accepted_count(R);
+    pos += 64;
+    g += na;
+    sg = rt_wrap<KGE64>(sg + na, K);
+    raw = nraw;
+}
+
+template <bool KGE64, typename JT>
 __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &pos, JT *__restrict__ J, uint32_t N,
                                                 uint32_t D, int lane) {
     const uint32_t K = N - 1;
@@ -411,43 +457,10 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         const int nrun = min((MT_N - pos + 63) >> 6, (int)((rem - 1u) >> 6));
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
-            for (int r = 0; r < nrun; r++) {
-                if (pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
-                    while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
-                    asm volatile("" ::: "memory");
-                    raw = kb[pos + lane];
-                }
-                // next window's words (after a crossing window: discarded by the block switch)
-                const uint32_t nraw = kb[pos + 64 + lane];
-                const uint32_t v = rt_temper_mask(raw, mK);
-                const uint64_t M = rt_window(rp.tbl, v, sg);
-                RP_STAMP(3);
-                // three evaluations without a convergence check (one more evaluation of
-                // the fixed point leaves it unchanged; ~5 are needed on average), then
-                // one per check: fewer VALU -> SALU round trips and branches
-                uint64_t R = ballot(rt_rej(M, s0));
-#pragma unroll
-                for (int e = 0; e < 3; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
-                uint32_t s;
-                int it = 4;
-                for (;;) {
-                    s = mbcnt_from(R, sbase);
-                    const uint64_t Rn = ballot(rt_rej(M, s));
-                    it++;
-                    if (Rn == R) break;
-                    R = Rn;
-                }
-                (void)it;
-                RP_STAMP(2);
-                RP_COUNT(5, 1);
-                RP_COUNT(6, it);
-                store_accepted(J, (g + 63u) - s, v, R);
-                const uint32_t na = accepted_count(R);
-                pos += 64;
-                g += na;
-                sg = rt_wrap(sg + na, K);
-                raw = nraw;
-            }
+            for (int r = 1; r < nrun; r++)
+                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, g, sg, J, K, mK, sbase, s0, lane);
+            tbl_window<true, KGE64>(rp, kb, blkno, pos, raw, g, sg, J, K, mK, sbase, s0, lane);
+            RP_STAMP(2);
             pre_pos = pos;
             pre_raw = raw;
             continue;
@@ -482,7 +495,7 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         if (na >= rem && na > 0) pos += fls64(A) + 1;
         else pos += nw;
         g += na;
-        sg = rt_wrap(sg + na, K);
+        sg = rt_wrap<KGE64>(sg + na, K);
     }
     rp.done_steps += G;
 }
