@@ -143,6 +143,7 @@ struct KArgs {
     uint8_t *spec_dirty_out;       // fix-up: scans replayed by this call (the next call's dirty_in)
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
+    int pts_global;     // chunk_kernel: Cartesian points read where they lie (no LDS copy)
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
     double *models;     // [n_chunks][T][4] 2-point models (origin, direction)
@@ -1290,11 +1291,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void sc
 // UKF step of the fused pipeline on groups of Pg lanes per scan (lslam_ukf.h: ukf_step_group),
 // after the association pass; the landmark slots [0, nchunks) take the scan's fitted chunk
 // origins (LMK_FROM_RANSAC) exactly as the post pass's corg does (models with LSLAM_VALID)
-__global__ __launch_bounds__(64) void ukf_group_kernel(const KArgs a, int Pg, int fuse) {
+__global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, int fuse) {
     const lslam_scan_batch &B = a.b;
-    const int lane = (int)threadIdx.x;
+    const int lane = (int)threadIdx.x & 63;
     const int g = lane & (Pg - 1);
-    const int s = (int)blockIdx.x * (64 / Pg) + lane / Pg;
+    const int wave = (int)blockIdx.x * (int)(blockDim.x >> 6) + ((int)threadIdx.x >> 6);
+    const int s = wave * (64 / Pg) + lane / Pg;
     WAVE_CENSUS(a, WC_UKF);
     const int uprio = (a.cons_prio & 256) ? (a.cons_prio >> 6) & 3 : (a.cons_prio >> 4) & 3;  // default: the post's
     if (uprio) set_prio_level(uprio);
@@ -1333,7 +1335,12 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
     int Pg = 1;
     while (Pg < (n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
     const int per = 64 / Pg;
-    hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((k.b.n_scans + per - 1) / per)), dim3(64), 0, stream, k, Pg,
+    // waves per workgroup (LSLAM_UKF_WG, 1..4): a workgroup's waves go to different SIMDs of one
+    // CU, so 4-wave groups keep the 253-VGPR waves at one per SIMD, where single-wave groups
+    // stack two on some SIMDs (full register file) and hold the next producer off that CU
+    static const int wpg = [] { const char *e = getenv("LSLAM_UKF_WG"); const int v = e ? atoi(e) : 4; return v >= 1 && v <= 4 ? v : 4; }();
+    const int nwaves = (k.b.n_scans + per - 1) / per;
+    hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((nwaves + wpg - 1) / wpg)), dim3(64 * wpg), 0, stream, k, Pg,
                        fuse ? 1 : 0);
 }
 
@@ -1954,7 +1961,7 @@ template <int HYP>
 __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned char *smem) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
-    double2 *P = (double2 *)(smem + a.off_pts);
+    double2 *Ps = (double2 *)(smem + a.off_pts);
     int32_t *draws = (int32_t *)(smem + a.off_draws);
     int32_t *cnt = (int32_t *)(smem + a.off_cnt);
     int32_t *tied = (int32_t *)(smem + a.off_tied);
@@ -1969,6 +1976,10 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
+    // Cartesian points are read where they lie when the layout holds no copy (pts_global):
+    // beside the producer every KiB of LDS per wave is consensus residency
+    const bool pg = a.pts_global && B.xy;
+    const double2 *P = pg ? (const double2 *)B.xy + p0 : Ps;
 #ifdef LSLAM_STAMPS
     unsigned long long *chdbg = a.dbg ? a.dbg + (size_t)c * 16 : nullptr;
 #else
@@ -2002,22 +2013,23 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     } else {
         const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
         dr = h;
-        if (N <= 128 && B.xy) {
+        if (pg) {
+        } else if (N <= 128 && B.xy) {
             double2 pv[2];
             const double2 *src = (const double2 *)B.xy + p0;
 #pragma unroll
             for (int k = 0; k < 2; k++) pv[k] = (lane + 64 * k < N) ? src[lane + 64 * k] : make_double2(0.0, 0.0);
 #pragma unroll
             for (int k = 0; k < 2; k++)
-                if (lane + 64 * k < N) P[lane + 64 * k] = pv[k];
+                if (lane + 64 * k < N) Ps[lane + 64 * k] = pv[k];
         } else {
-            stage_points(B, p0, N, P, lane);
+            stage_points(B, p0, N, Ps, lane);
         }
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
     }
     CH_STAMP(0);
-    if (HYP == LSLAM_HYP_PHILOX) stage_points(B, p0, N, P, lane);
+    if (HYP == LSLAM_HYP_PHILOX && !pg) stage_points(B, p0, N, Ps, lane);
     __syncthreads();
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
@@ -3237,7 +3249,7 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
     const int T = k.T;
     int off = 0;
-    k.off_pts = off; off += align16(16 * N);
+    k.off_pts = off; off += k.pts_global ? 0 : align16(16 * N);
     k.off_draws = off; off += (k.hyp_source == LSLAM_HYP_PHILOX) ? align16(8 * (T + 1)) : 0;  // else read in place
     k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
@@ -3421,6 +3433,11 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     const int ppw = c->rng_ppw;
     int st = layout_rng(k, &k.b, lds, ppw);
     if (st) return st;
+    // at least this much LDS per producer workgroup (LSLAM_RNG_LDS_MIN): above 32 KiB a CU holds
+    // at most 4 of them, so a workgroup that finds its CU busy waits for it instead of landing
+    // as a fifth on another CU (5 parsers per SIMD there: the whole launch 20-30 % longer)
+    static const int lds_min = [] { const char *e = getenv("LSLAM_RNG_LDS_MIN"); return e ? atoi(e) : 0; }();
+    if (lds < lds_min && lds_min <= 160 * 1024) lds = lds_min;
     static std::once_flag once;
     std::call_once(once, [] {
         set_max_lds(rng_kernel<uint8_t, 1>);
@@ -3655,6 +3672,8 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
         return timer_end(c, LSLAM_K_CONSENSUS);
     }
     int lds = 0;
+    static const bool gpts = [] { const char *e = getenv("LSLAM_CHUNK_GPTS"); return e && atoi(e) != 0; }();
+    k.pts_global = (gpts && k.b.xy) ? 1 : 0;
     st = layout_chunk(k, &k.b, lds);
     if (st) return st;
     static std::once_flag once;
@@ -3800,6 +3819,9 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     // behind the fix-up runs alone (35 us) instead of beside the parsers (~180 us): C3
     // 0.893 -> 0.858 ms per step, the producer 0.79 -> 0.71 ms in the pipeline
     static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 3; }();
+    // the slot's release event after the whole call (next to ev_call) instead of right after the
+    // fix-up: one marker packet fewer inside the ctx chain (A/B: LSLAM_SLOT_AT_END)
+    static const bool slot_at_end = [] { const char *e = getenv("LSLAM_SLOT_AT_END"); return e && atoi(e) != 0; }();
     const bool ukf_indep = ukf_lane && !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
     const int ukf_at = ukf_indep ? ukf_early : 0;
     if (ukf_lane && ukf_at == 2) {
@@ -3841,7 +3863,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_fix,
                            c->stream, kf);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+        if (!slot_at_end) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     }
     if (ukf_lane && ukf_at == 3) {
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
@@ -3869,6 +3891,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         HIPCHK(hipGetLastError());
     }
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
+    if (mt && slot_at_end) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_PIPELINE);
