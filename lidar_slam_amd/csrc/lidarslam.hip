@@ -2842,7 +2842,7 @@ int lslam_h2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
     if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
+    // (the previous calls, which may still read dst, are ahead of this on the ctx stream)
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     note_copy(c, dst, n);
@@ -2853,8 +2853,7 @@ int lslam_d2h(lslam_ctx *c, void *dst, const void *src, size_t n) {
     if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
-    // after every pipeline call so far, whichever of the context's streams ran its last pass
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));
+    // (the previous calls, which may still read dst, are ahead of this on the ctx stream)
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
     return LSLAM_OK;
 }
@@ -2863,7 +2862,7 @@ int lslam_d2d(lslam_ctx *c, void *dst, const void *src, size_t n) {
     if (!c || (!dst && n) || (!src && n)) return LSLAM_ERR_ARG;
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
+    // (the previous calls, which may still read dst, are ahead of this on the ctx stream)
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     note_copy(c, dst, n);
@@ -2905,7 +2904,7 @@ int lslam_memset(lslam_ctx *c, void *dst, int v, size_t n) {
     if (!c || (!dst && n)) return LSLAM_ERR_ARG;
     if (!n) return LSLAM_OK;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_call, 0));  // the previous call may still read dst
+    // (the previous calls, which may still read dst, are ahead of this on the ctx stream)
     HIPCHK(hipMemsetAsync(dst, v, n, c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     note_copy(c, dst, n);
@@ -3567,9 +3566,17 @@ static void remember_outputs(lslam_ctx *c, const lslam_scan_batch *b, int T, int
     for (int i = 0; i < 11; i++) note_out(c, p[i], n[i]);
 }
 
-// every entry point that enqueues device work ends here: later calls order against ev_call
-// (h2d / d2h / memset, the side-stream UKF and, on a hazard, the next MT producer)
+// Every entry point that enqueues device work ends here.  Each call's work on the producer
+// and side streams joins the ctx stream before the call returns, so "every call so far" is the
+// ctx stream's tail: copies on the ctx stream follow it by stream order, and another stream
+// that must wait for it records ev_call at that moment (mark_calls) and waits on that.  An
+// event recorded at every call's end would be a marker packet inside the pipelined ctx chain
+// (~7 us between two kernels on the MI355X).
 static int end_call(lslam_ctx *c) {
+    (void)c;
+    return LSLAM_OK;
+}
+static int mark_calls(lslam_ctx *c) {
     HIPCHK(hipEventRecord(c->ev_call, c->stream));
     return LSLAM_OK;
 }
@@ -3766,6 +3773,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (st) return st;
     if (ukf_side) {
         // after the previous call (its outputs may be this step's inputs) and the latest copies
+        if ((st = mark_calls(c))) return st;
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_call, 0));
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_copy, 0));
         if (c->ukf_lanes) {
@@ -3791,6 +3799,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         const int hz = producer_hazard(c, b);
         if (hz == 2) {
             // ev_call follows every call enqueued so far: the union starts afresh
+            if ((st = mark_calls(c))) return st;
             HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_call, 0));
             c->n_out = 0;
             c->out_unknown = 0;
