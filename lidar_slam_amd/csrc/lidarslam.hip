@@ -3828,9 +3828,10 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     // behind the fix-up runs alone (35 us) instead of beside the parsers (~180 us): C3
     // 0.893 -> 0.858 ms per step, the producer 0.79 -> 0.71 ms in the pipeline
     static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 3; }();
-    // the slot's release event after the whole call (next to ev_call) instead of right after the
-    // fix-up: one marker packet fewer inside the ctx chain (A/B: LSLAM_SLOT_AT_END)
-    static const bool slot_at_end = [] { const char *e = getenv("LSLAM_SLOT_AT_END"); return e && atoi(e) != 0; }();
+    // where the slot's release event (the next producer's start) goes in the ctx chain
+    // (LSLAM_SLOT_AT): 0 = right after the fix-up (default), 1 = after the post pass (before a
+    // UKF placed after it), 2 = at the end of the call
+    static const int slot_at = [] { const char *e = getenv("LSLAM_SLOT_AT"); return e ? atoi(e) : 0; }();
     const bool ukf_indep = ukf_lane && !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
     const int ukf_at = ukf_indep ? ukf_early : 0;
     if (ukf_lane && ukf_at == 2) {
@@ -3872,7 +3873,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_fix,
                            c->stream, kf);
         HIPCHK(hipGetLastError());
-        if (!slot_at_end) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+        if (slot_at != 1 && slot_at != 2) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     }
     if (ukf_lane && ukf_at == 3) {
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
@@ -3895,12 +3896,13 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
+    if (mt && slot_at == 1) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     if (ukf_lane && ukf_at == 0) {
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
         HIPCHK(hipGetLastError());
     }
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
-    if (mt && slot_at_end) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+    if (mt && slot_at == 2) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_PIPELINE);
