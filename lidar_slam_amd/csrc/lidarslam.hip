@@ -1368,6 +1368,7 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         rp.fl = (lds_flag_t *)(base + a.off_fl);
         rp.tbl = (uint32_t *)(base + a.off_tbl);
         rp.tblK = 0;
+        rp.self_twist = blockDim.x == 64u * PPW;  // launched without the helper wave
         return rp;
     };
     // Shared reject tables (off_stbl >= 0): the workgroup's parsers claim up to two table Ks
@@ -3446,7 +3447,11 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     });
     st = timer_begin(c, LSLAM_K_RNG, stream);
     if (st) return st;
-    const dim3 grid((unsigned)((k.b.n_scans + ppw - 1) / ppw)), block(64 * (ppw + 1));
+    // No helper wave by default: each parser twists its own next block when it needs it (its chain
+    // ~3 % longer), so the producer holds 4 instead of 5 waves per SIMD and the consumers beside it
+    // one more: C3 0.855 -> 0.839 ms per step.  LSLAM_RNG_SELF=0: the helper wave twists ahead.
+    static const bool self_tw = [] { const char *e = getenv("LSLAM_RNG_SELF"); return !(e && atoi(e) == 0); }();
+    const dim3 grid((unsigned)((k.b.n_scans + ppw - 1) / ppw)), block(64 * (ppw + (self_tw ? 0 : 1)));
     if (ppw == 4) {
         if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t, 4>), grid, block, lds, stream, k);
         else hipLaunchKernelGGL((rng_kernel<uint16_t, 4>), grid, block, lds, stream, k);

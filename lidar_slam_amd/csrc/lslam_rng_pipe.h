@@ -129,6 +129,7 @@ struct RngPipe {
     uint32_t lvl_t1, lvl_t2;  // parser: done steps at which the level drops (rp_set_schedule)
     uint32_t done_steps;   // parser: steps of the finished chunks
     int prio;              // parser: current priority level
+    bool self_twist;       // no helper wave: the parser twists each block itself when it needs it
 #ifdef LSLAM_STAMPS
     uint64_t acc[8];
 #endif
@@ -142,6 +143,24 @@ __device__ __forceinline__ void rp_set_schedule(RngPipe &rp) {
 }
 __device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done) {
     return RP_PRIO_TOP - (done >= rp.lvl_t1 ? 1 : 0) - (done >= rp.lvl_t2 ? 1 : 0);
+}
+
+// Block `need` of the pipe, before the parser reads it: from the helper wave (its flag), or
+// twisted by the parser itself (self_twist: block need - 1 -> slot need & 1, which held block
+// need - 2, already parsed; an even block also refreshes the pad after slot 1).
+__device__ __forceinline__ void rp_need_block(RngPipe &rp, int need, int lane) {
+    if (rp.self_twist) {
+        if (lds_flag_get(rp.fl + F_BLK) < need) {
+            mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N, lane);
+            if ((need & 1) == 0) {
+                rp.blk[2 * MT_N + lane] = rp.blk[lane];
+                wave_lds_sync();
+            }
+            lds_flag_put(rp.fl + F_BLK, need);
+        }
+        return;
+    }
+    while (lds_flag_get(rp.fl + F_BLK) < need) __builtin_amdgcn_s_sleep(1);
 }
 
 // Diagnostic build only: parser cycle accounting (0 block waits, 2 fixed point,
@@ -220,7 +239,7 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
         RP_STAMP(3);
         if (pos >= MT_N) {
             blkno += 1;
-            while (lds_flag_get(rp.fl + F_BLK) < blkno) __builtin_amdgcn_s_sleep(1);
+            rp_need_block(rp, blkno, lane);
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
@@ -388,7 +407,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
                                            uint32_t &g, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
                                            uint32_t sbase, uint32_t s0, int lane) {
     if (CHECK && pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
-        while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
+        rp_need_block(rp, blkno + 1, lane);
         asm volatile("" ::: "memory");
         raw = kb[pos + lane];
     }
@@ -436,7 +455,7 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         RP_STAMP(3);
         if (pos >= MT_N) {
             blkno += 1;
-            while (lds_flag_get(rp.fl + F_BLK) < blkno) __builtin_amdgcn_s_sleep(1);
+            rp_need_block(rp, blkno, lane);
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
@@ -468,7 +487,7 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         // ---- the chunk's last window (rem <= 64), possibly across the block boundary.
         // A = accept ballot (lanes whose count is below rem); ~A counts the others as rejected.
         if (pos + 64 > MT_N) {
-            while (lds_flag_get(rp.fl + F_BLK) < blkno + 1) __builtin_amdgcn_s_sleep(1);
+            rp_need_block(rp, blkno + 1, lane);
             asm volatile("" ::: "memory");
             pre_pos = -1;
         }
