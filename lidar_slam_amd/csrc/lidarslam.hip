@@ -144,6 +144,7 @@ struct KArgs {
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     int pts_global;     // chunk_kernel: Cartesian points read where they lie (no LDS copy)
+    int lmk_reg;        // post pass (association only, lmk_cap <= 64): landmark list in registers
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
     double *models;     // [n_chunks][T][4] 2-point models (origin, direction)
@@ -931,6 +932,200 @@ __device__ void post_assoc_fast(const KArgs &a, int s, int c0, int nchunks, int 
 }
 
 // ------------------------------------------------------------------------
+// The same post pass with the scan's landmark list in registers (lmk_cap <= 64: entry i in
+// lane i).  Beside the next call's producer the post pass was bound by its LDS (4.8 KiB per
+// wave, 3.6 of them the list: ~9 waves per CU); here it holds 1.2 KiB.  The walk is the same
+// bit operations on the same ballots (associate), removal is a compaction by ds_permute (kept
+// entries to their rank, removed ones above the new length), the matched entry's line is read
+// with a lane shuffle before the list changes.  Same values, same list order.
+// ------------------------------------------------------------------------
+struct LmkReg {
+    double a, b, px, py, ex, ey;
+    int id, life;
+};
+
+__device__ __forceinline__ bool is_equal_reg(const LmkReg &Lk, double a, double b, double px, double py, double ex,
+                                             double ey, const KArgs &ka) {
+    const double distA = fabs(Lk.a - a);
+    const double distB = fabs(Lk.b - b);
+    const double vx = Lk.ex - px, vy = Lk.ey - py;
+    const double dEO = cr_sqrt(__builtin_fma(vy, vy, vx * vx));
+    const double wx = Lk.px - ex, wy = Lk.py - ey;
+    const double dOE = cr_sqrt(__builtin_fma(wy, wy, wx * wx));
+    if (distA <= ka.tol_a && distB <= ka.tol_b) return (dEO <= ka.tol_dist || dOE <= ka.tol_dist);
+    return false;
+}
+
+__device__ __forceinline__ double permute_d(int addr, double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_permute(addr, (int)(unsigned)u);
+    const int hi = __builtin_amdgcn_ds_permute(addr, (int)(unsigned)(u >> 32));
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ int associate_reg(const KArgs &ka, LmkReg &e, int &L, double a, double b, double px, double py, double ex,
+                             double ey, int id, double &pa, double &pb, bool &overflow, int32_t *walk_out, int lane) {
+    const bool have = lane < L;
+    bool eq = false, dies = false;
+    if (have) {
+        eq = is_equal_reg(e, a, b, px, py, ex, ey, ka);
+        dies = e.life <= 1;
+    }
+    const uint64_t E = ballot(eq);
+    const uint64_t D = ballot(dies);
+    // the walk of associate() for one block starting at position 0 (see the comment there)
+    int match = -1;
+    uint64_t V = 0ull;
+    if (L > 0) {
+        const uint64_t valid = L >= 64 ? ~0ull : ((1ull << L) - 1ull);
+        const uint64_t Dm = D & valid;
+        const uint64_t run0 = Dm & ~(Dm << 1);
+        const uint64_t EVEN = 0x5555555555555555ull;
+        const uint64_t Re = Dm & ~(Dm + (run0 & EVEN));
+        const uint64_t EO = (Re & EVEN) | (Dm & ~Re & ~EVEN);
+        const uint64_t visited = valid & ~(EO << 1);
+        const uint64_t hits = visited & E;
+        V = visited;
+        if (hits) {
+            const int m = ffs64(hits);
+            match = m;
+            V = visited & ((1ull << m) - 1ull);
+        }
+    }
+    pa = a;
+    pb = b;
+    if (match >= 0) {
+        pa = unid(__shfl(e.a, match));
+        pb = unid(__shfl(e.b, match));
+    }
+    // decrease_life / removal / reset_life, then compaction in list order
+    bool keep = false;
+    if (have) {
+        if ((V >> lane) & 1ull) {
+            if (e.life > 0) e.life -= 1;
+            keep = e.life != 0;
+        } else {
+            keep = true;
+        }
+        if (lane == match) e.life = ka.life;
+        if (walk_out) walk_out[lane] = e.life;
+    }
+    const uint64_t km = ballot(keep);
+    const int nL = popc64(km);
+    if (nL != L) {  // something was removed: kept entries to their rank, the others above nL
+        const int dst = keep ? (int)mbcnt(km) : nL + (int)mbcnt(~km);
+        const int ad = dst << 2;
+        e.a = permute_d(ad, e.a);
+        e.b = permute_d(ad, e.b);
+        e.px = permute_d(ad, e.px);
+        e.py = permute_d(ad, e.py);
+        e.ex = permute_d(ad, e.ex);
+        e.ey = permute_d(ad, e.ey);
+        e.id = __builtin_amdgcn_ds_permute(ad, e.id);
+        e.life = __builtin_amdgcn_ds_permute(ad, e.life);
+    }
+    L = nL;
+    overflow = false;
+    if (match < 0) {
+        if (L < ka.lmk_cap) {
+            if (lane == L) {
+                e.a = a; e.b = b; e.px = px; e.py = py; e.ex = ex; e.ey = ey;
+                e.id = id; e.life = ka.life;
+            }
+            L += 1;
+        } else {
+            overflow = true;
+        }
+    }
+    return match;
+}
+
+__device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, int lane) {
+    const lslam_scan_batch &B = a.b;
+    const int c0 = B.scan_chunk_off[s], nchunks = B.scan_chunk_off[s + 1] - c0;
+    const int id0 = B.id_base ? B.id_base[s] : 0;
+    lslam_chunk_model *recs = (lslam_chunk_model *)rbuf;
+    int32_t *off = (int32_t *)(rbuf + (((int)sizeof(lslam_chunk_model) * a.hist_cap + 15) & ~15));
+    {
+        const uint4 *src = (const uint4 *)(B.models + c0);
+        uint4 *dst = (uint4 *)rbuf;
+        for (int e = lane; e < nchunks * 7; e += 64) dst[e] = src[e];
+        for (int e = lane; e <= nchunks; e += 64) off[e] = B.chunk_pt_off[c0 + e];
+    }
+    int L = min(uni(B.lmk_count[s]), a.lmk_cap);
+    lslam_landmark *lst = B.landmarks + (size_t)s * a.lmk_cap;
+    LmkReg e;
+    if (lane < L) {
+        const lslam_landmark g = lst[lane];
+        e.a = g.a; e.b = g.b; e.px = g.pos_x; e.py = g.pos_y; e.ex = g.end_x; e.ey = g.end_y;
+        e.id = g.id; e.life = g.life;
+    } else {
+        e.a = e.b = e.px = e.py = e.ex = e.ey = 0.0;
+        e.id = 0;
+        e.life = 0;
+    }
+    __syncthreads();
+    int32_t *walk = B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr;
+    for (int ci = 0; ci < nchunks; ci++) {
+        lslam_chunk_model rec = recs[ci];
+        rec.landmark_id = id0 + ci;
+        if (rec.flags & LSLAM_VALID) {
+            double pa, pb;
+            bool overflow = false;
+            const int m = associate_reg(a, e, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
+                                        rec.landmark_id, pa, pb, overflow, walk, lane);
+            rec.match_index = m;
+            rec.proj_a = pa;
+            rec.proj_b = pb;
+            rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
+            if (overflow) rec.flags |= LSLAM_CAPACITY;
+        }
+        __syncthreads();  // every lane has its copy of recs[ci]
+        if (lane == 0) recs[ci] = rec;
+    }
+    if (lane < L) {
+        lslam_landmark g;
+        g.a = e.a; g.b = e.b; g.pos_x = e.px; g.pos_y = e.py; g.end_x = e.ex; g.end_y = e.ey;
+        g.id = e.id; g.life = e.life;
+        lst[lane] = g;
+    }
+    if (lane == 0) B.lmk_count[s] = L;
+    __syncthreads();
+    {
+        const uint4 *src = (const uint4 *)rbuf;
+        uint4 *dst = (uint4 *)(B.models + c0);
+        for (int k = lane; k < nchunks * 7; k += 64) dst[k] = src[k];
+    }
+    if (!B.y_proj) return;
+    const int q0 = off[0], q1 = off[nchunks];
+    int ci = 0;
+    for (int qb = q0; qb < q1; qb += 4 * 64) {
+        uint8_t mk[4];
+        double xs[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = qb + u * 64 + lane;
+            mk[u] = 0;
+            xs[u] = 0.0;
+            if (q < q1) {
+                mk[u] = B.inlier_mask[q];
+                xs[u] = B.xy ? B.xy[2 * (size_t)q] : polar_xy(B.theta_deg[q], B.dist_mm[q]).x;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = qb + u * 64 + lane;
+            if (q < q1) {
+                while (ci + 1 < nchunks && off[ci + 1] <= q) ci++;
+                const lslam_chunk_model &r = recs[ci];
+                const bool have_model = (r.flags & LSLAM_VALID) != 0;
+                B.y_proj[q] = (have_model && mk[u]) ? (r.proj_a * xs[u] + r.proj_b) : 0.0;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
 // the scan kernel
 // ------------------------------------------------------------------------
 template <int HYP, int MODE>
@@ -1003,6 +1198,12 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 
     if (use_mt) mt_init();
 
+    if constexpr (kPost && (MODE & MODE_ASSOC) != 0 && (MODE & MODE_UKF) == 0) {
+        if (a.lmk_reg) {  // the list in registers (association-only post pass, lmk_cap <= 64)
+            post_assoc_reg(a, s, smem + a.off_recs, lane);
+            return;
+        }
+    }
     // landmark list of this scan -> LDS
     int L = 0;
     if (MODE & MODE_ASSOC) {
@@ -3168,8 +3369,12 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     k.off_zobs = off; off += (u && (u->flags & LSLAM_UKF_MAP)) ? align16(16 * k.corg_cap) : 0;
     k.lmk_cap = (mode & MODE_ASSOC) ? b->lmk_capacity : 0;
     if ((mode & MODE_ASSOC) && k.lmk_cap <= 0) return set_err(LSLAM_ERR_ARG, "lmk_capacity must be > 0");
-    k.off_lmk = off; off += align16((int)sizeof(lslam_landmark) * (k.lmk_cap > 0 ? k.lmk_cap : 1));
-    k.off_vis = off; off += align16(8 * ((k.lmk_cap + 63) / 64 + 1));
+    // the association-only post pass keeps a list of at most 64 entries in registers
+    static const bool lmk_reg_on = [] { const char *e = getenv("LSLAM_LMK_REG"); return !(e && atoi(e) == 0); }();
+    k.lmk_reg = (lmk_reg_on && mode == MODE_ASSOC && k.lmk_cap > 0 && k.lmk_cap <= 64 && k.off_recs >= 0 &&
+                 !(u && (u->flags & LSLAM_UKF_MAP)) && b->landmarks) ? 1 : 0;
+    k.off_lmk = off; off += k.lmk_reg ? 0 : align16((int)sizeof(lslam_landmark) * (k.lmk_cap > 0 ? k.lmk_cap : 1));
+    k.off_vis = off; off += k.lmk_reg ? 0 : align16(8 * ((k.lmk_cap + 63) / 64 + 1));
     k.pts_cap = N;
     if (u) {
         if (u->n_landmarks <= 0) return set_err(LSLAM_ERR_ARG, "n_landmarks must be > 0");
