@@ -166,7 +166,13 @@ def landmark_extraction(xy, landmark_number, landmarks, state, thr=20.0, trials=
     rc = lib().or_landmark_extraction(_p(xy, C.c_double), n, int(landmark_number), float(thr), int(trials),
                                       _p(state.key, C.c_uint32), C.byref(state.pos), arr, C.byref(count),
                                       cap, _p(mask, C.c_uint8), _p(yproj, C.c_double), C.byref(m))
-    if rc != 0:
+    if rc == -2:
+        # no match and the list was full (the library's LSLAM_CAPACITY): the chunk's landmark is
+        # dropped, its inliers projected on its own line (or_associate left proj_a/b = a, b)
+        m.flags |= 64 | 256
+        m.match_index = -1
+        yproj[:n] = np.where(mask[:n] != 0, m.proj_a * xy[:, 0] + m.proj_b, 0.0)
+    elif rc != 0:
         raise RuntimeError("oracle landmark_extraction rc=%d" % rc)
     return mask[:n], yproj[:n], model_dict(m), array_to_landmarks(arr, count.value)
 

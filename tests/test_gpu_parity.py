@@ -544,3 +544,76 @@ def test_batch256_pipeline_vs_reference(ctx, golden):
         st = r["mt_state"][s]
         h = int.from_bytes(hashlib.sha256(st[:624].tobytes() + np.int32(st[624]).tobytes()).digest()[:8], "little")
         assert h == int(g["state_after_hash"][s]), s
+
+
+@pytest.mark.parametrize("cap", [64, 24])
+def test_assoc_lists_stress_vs_oracle(ctx, cap):
+    """The association-only post pass (its landmark list in registers when lmk_capacity <= 64,
+    post_assoc_reg) against the oracle's chained landmark_extraction
+    (ransac_functions.py:15-59, landmarking.py:48-77): input lists of 0..cap entries mixing
+    near-copies of the scan's own walls (matches), junk lines and lives of 1..3 (runs of
+    removals, skip-after-remove), full lists (a new landmark dropped: LSLAM_CAPACITY).  Final
+    lists (ids, lives, lines), per-chunk new/matched/capacity flags and y_proj exact."""
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import LANDMARK_DTYPE, ScanPipeline
+    S = 48
+    ids = list(range(300, 300 + S))
+    b = synth.make_batch(ids, 720)
+    xy, sco, cpo = b["xy"], b["scan_chunk_off"], b["chunk_pt_off"]
+    rng = np.random.default_rng(7)
+    # the scans' own fitted walls (oracle, empty lists) seed plausible matches
+    walls = []
+    for s in range(S):
+        st = orc.MTState(seed=s)
+        ws = []
+        for k, c in enumerate(range(sco[s], sco[s + 1])):
+            _, _, mod, _ = orc.landmark_extraction(xy[cpo[c]:cpo[c + 1]], k, [], st, cap=1)
+            if mod["flags"] & 1:
+                ws.append(mod)
+        walls.append(ws)
+    lm = np.zeros((S, cap), LANDMARK_DTYPE)
+    cnt = np.zeros(S, np.int32)
+    lists_in = []
+    for s in range(S):
+        full = s % 5 == 0  # a full list of long-lived junk: nothing matches or dies, nothing fits
+        n = cap if full else int(rng.integers(0, cap + 1))
+        lst = []
+        for i in range(n):
+            if walls[s] and not full and rng.random() < 0.5:
+                w = walls[s][int(rng.integers(len(walls[s])))]
+                a, bb = w["a"] + rng.normal(0, 0.01), w["b"] + rng.normal(0, 2.0)
+                pos, end = (w["ox"], w["oy"]), (w["tip_x"], w["tip_y"])
+            else:
+                a, bb = rng.normal(0, 3), rng.normal(0, 3000)
+                pos, end = tuple(rng.uniform(-5000, 5000, 2)), tuple(rng.uniform(-5000, 5000, 2))
+            life = 40 if full else int(rng.choice([1, 1, 2, 3, 40]))
+            lst.append({"a": float(a), "b": float(bb), "pos": (float(pos[0]), float(pos[1])),
+                        "end": (float(end[0]), float(end[1])), "id": 5000 + i, "life": life})
+        lists_in.append(lst)
+        cnt[s] = n
+        for i, L in enumerate(lst):
+            lm[s, i] = (L["a"], L["b"], L["pos"][0], L["pos"][1], L["end"][0], L["end"][1], L["id"], L["life"])
+    id_base = (np.arange(S) * 100).astype(np.int32)
+    p = ScanPipeline(ctx, xy, sco, cpo, seeds=np.arange(S, dtype=np.uint32), landmarks=lm, lmk_count=cnt,
+                     lmk_capacity=cap, id_base=id_base)
+    p.run()
+    r = p.results()
+    m = r["models"]
+    n_cap = 0
+    for s in range(S):
+        st = orc.MTState(seed=s)
+        lst = [dict(L) for L in lists_in[s]]
+        for k, c in enumerate(range(sco[s], sco[s + 1])):
+            p0, p1 = cpo[c], cpo[c + 1]
+            mask, yp, mod, lst = orc.landmark_extraction(xy[p0:p1], int(id_base[s]) + k, lst, st, cap=cap)
+            assert np.array_equal(r["mask"][p0:p1], mask), (s, k)
+            assert np.array_equal(r["y_proj"][p0:p1], yp), (s, k)
+            for f in (64, 128, 256):
+                assert bool(m["flags"][c] & f) == bool(mod["flags"] & f), (s, k, f)
+            n_cap += bool(m["flags"][c] & 256)
+        got = r["landmarks"][s, :r["lmk_count"][s]]
+        assert r["lmk_count"][s] == len(lst), s
+        assert list(got["id"]) == [L["id"] for L in lst], s
+        assert list(got["life"]) == [L["life"] for L in lst], s
+        assert np.array_equal(got["a"], [L["a"] for L in lst]) and np.array_equal(got["end_y"], [L["end"][1] for L in lst])
+    assert n_cap > 0  # the full-list case was exercised
