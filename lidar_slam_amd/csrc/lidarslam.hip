@@ -1816,6 +1816,10 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
 // i at byte K - i); the lowest group may start up to 15 bytes before the row (the
 // previous row, or the slot's front pad JBUF_FRONT) and walks only i <= K.
 constexpr int RR_GROUPS = 8;  // K <= 127
+#ifndef LSLAM_RR_FAST
+#define LSLAM_RR_FAST 1
+#endif
+constexpr bool RR_FAST = LSLAM_RR_FAST != 0;  // 5-VALU steps for i <= 64 (rr_step_nx)
 constexpr size_t JBUF_FRONT = 64;  // bytes of a producer slot before its steps
 // One step of both trackers, c = (j == c) ? i : c.  The two trackers are independent
 // chains, so both compares are issued (masks in two SGPR pairs) before both selects; the
@@ -1853,16 +1857,67 @@ __device__ __forceinline__ void rr_walk_from(const uint32_t (&w)[4], uint32_t K,
     }
 }
 
+// Steps i <= 64: i is an inline constant of the selects, so no v_mov is needed; the next
+// step's byte extract (independent of the trackers) stands between the compares and the
+// selects as the second wait state: 5 VALU per step instead of 6.
+template <uint32_t I>
+__device__ __forceinline__ void rr_step_nx(uint32_t j, uint32_t &c0, uint32_t &c1, uint32_t &jn, uint32_t wn) {
+    static_assert(I >= 2 && I < 64, "inline-constant step");
+    constexpr int offn = 15 - (int)((I % 16u));        // byte of step I + 1 within its group
+    constexpr uint32_t nbn = 32u - (uint32_t)__builtin_clz(I + 1u);
+    uint64_t m0, m1;
+    asm volatile(
+        "v_cmp_eq_u32_e64 %[m0], %[j], %[c0]\n\t"
+        "v_cmp_eq_u32_e64 %[m1], %[j], %[c1]\n\t"
+        "v_bfe_u32 %[jn], %[wn], %[off], %[nb]\n\t"
+        "v_cndmask_b32_e64 %[c0], %[c0], %[i], %[m0]\n\t"
+        "v_cndmask_b32_e64 %[c1], %[c1], %[i], %[m1]"
+        : [c0] "+v"(c0), [c1] "+v"(c1), [m0] "=&s"(m0), [m1] "=&s"(m1), [jn] "=&v"(jn)
+        : [j] "v"(j), [wn] "v"(wn), [off] "i"(8 * (offn & 3)), [nb] "i"(nbn), [i] "i"(I));
+}
+
+// group T <= 3 (steps 16T+1 .. 16T+16 <= 64), j of the current step given
+template <bool CHECK, uint32_t T, int U>
+__device__ __forceinline__ void rr_walk_fast(const uint32_t (&w)[4], uint32_t K, uint32_t &c0, uint32_t &c1, uint32_t j) {
+    if constexpr (U < 16) {
+        constexpr uint32_t i = 16u * T + 1u + (uint32_t)U;
+        if (CHECK && i > K) return;
+        if constexpr (U < 15) {
+            constexpr int offn = 15 - (U + 1);
+            uint32_t jn;
+            if constexpr (i >= 2u) {
+                rr_step_nx<i>(j, c0, c1, jn, w[offn >> 2]);
+            } else {  // step 1 decides the final swap, not a tracker step
+                jn = __builtin_amdgcn_ubfe(w[offn >> 2], (uint32_t)(8 * (offn & 3)), 32u - (uint32_t)__builtin_clz(i + 1u));
+            }
+            rr_walk_fast<CHECK, T, U + 1>(w, K, c0, c1, jn);
+        } else {
+            rr_step<i>(j, c0, c1);
+        }
+    }
+}
+
+template <bool CHECK, uint32_t T>
+__device__ __forceinline__ void rr_walk_group(const uint32_t (&ws)[4], uint32_t K, uint32_t &c0, uint32_t &c1) {
+    if constexpr (T <= 3u && RR_FAST) {
+        constexpr uint32_t i0 = 16u * T + 1u;
+        const uint32_t j0 = __builtin_amdgcn_ubfe(ws[3], 24u, 32u - (uint32_t)__builtin_clz(i0));  // byte 15
+        rr_walk_fast<CHECK, T, 0>(ws, K, c0, c1, j0);
+    } else {
+        rr_walk_from<CHECK, T, 0>(ws, K, c0, c1);
+    }
+}
+
 template <uint32_t T>
 __device__ __forceinline__ void rr_walk_groups(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t nfull, uint32_t &c0,
                                                uint32_t &c1) {
     if constexpr (T < (uint32_t)RR_GROUPS) {
         const uint32_t ws[4] = {w[T].x, w[T].y, w[T].z, w[T].w};
         if (T < nfull) {
-            rr_walk_from<false, T, 0>(ws, K, c0, c1);
+            rr_walk_group<false, T>(ws, K, c0, c1);
             rr_walk_groups<T + 1>(w, K, nfull, c0, c1);
         } else if (T == nfull) {
-            rr_walk_from<true, T, 0>(ws, K, c0, c1);
+            rr_walk_group<true, T>(ws, K, c0, c1);
         }
     }
 }
