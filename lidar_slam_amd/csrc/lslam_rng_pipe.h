@@ -243,8 +243,10 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            lds_flag_put(rp.fl + F_BLKUSE, blkno);
-            wake_helper();
+            if (!rp.self_twist) {
+                lds_flag_put(rp.fl + F_BLKUSE, blkno);
+                wake_helper();
+            }
             const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;
@@ -402,9 +404,10 @@ __device__ __forceinline__ void rt_load(RngPipe &rp, const uint32_t *__restrict_
 // One full table-mode window (64 words, short of the chunk's end).  Only the last window of a
 // run may run across the block's end (CHECK): the others skip that test, so the run loop
 // carries one backward branch per window.
+// gq = g + 63 (steps of the chunk before this window, + 63): lane l's step is gq - s_l.
 template <bool CHECK, bool KGE64, typename JT>
 __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int blkno, int &pos, uint32_t &raw,
-                                           uint32_t &g, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
+                                           uint32_t &gq, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
                                            uint32_t sbase, uint32_t s0, int lane) {
     if (CHECK && pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
         rp_need_block(rp, blkno + 1, lane);
@@ -431,10 +434,10 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
         R = Rn;
     }
     RP_COUNT(5, 1);
-    store_accepted(J, (g + 63u) - s, v, R);
+    store_accepted(J, gq - s, v, R);
     const uint32_t na = accepted_count(R);
     pos += 64;
-    g += na;
+    gq += na;
     sg = rt_wrap<KGE64>(sg + na, K);
     raw = nraw;
 }
@@ -459,8 +462,10 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            lds_flag_put(rp.fl + F_BLKUSE, blkno);
-            wake_helper();
+            if (!rp.self_twist) {
+                lds_flag_put(rp.fl + F_BLKUSE, blkno);
+                wake_helper();
+            }
             const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;
@@ -476,9 +481,12 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
         const int nrun = min((MT_N - pos + 63) >> 6, (int)((rem - 1u) >> 6));
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
-            for (int r = 1; r < nrun; r++)
-                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, g, sg, J, K, mK, sbase, s0, lane);
-            tbl_window<true, KGE64>(rp, kb, blkno, pos, raw, g, sg, J, K, mK, sbase, s0, lane);
+            uint32_t gq = g + 63u;
+            const int pos_last = pos + 64 * (nrun - 1);  // the run's last window (the only CHECK one)
+            while (pos != pos_last)
+                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            tbl_window<true, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            g = gq - 63u;
             RP_STAMP(2);
             pre_pos = pos;
             pre_raw = raw;
