@@ -143,7 +143,6 @@ struct KArgs {
     uint8_t *spec_dirty_out;       // fix-up: scans replayed by this call (the next call's dirty_in)
     int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
-    int pts_global;     // chunk_kernel: Cartesian points read where they lie (no LDS copy)
     int lmk_reg;        // post pass (association only, lmk_cap <= 64): landmark list in registers
     // large chunks (N > 128): count_kernel -> select_kernel
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
@@ -2218,7 +2217,7 @@ template <int HYP>
 __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned char *smem) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
-    double2 *Ps = (double2 *)(smem + a.off_pts);
+    double2 *P = (double2 *)(smem + a.off_pts);
     int32_t *draws = (int32_t *)(smem + a.off_draws);
     int32_t *cnt = (int32_t *)(smem + a.off_cnt);
     int32_t *tied = (int32_t *)(smem + a.off_tied);
@@ -2233,10 +2232,6 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
-    // Cartesian points are read where they lie when the layout holds no copy (pts_global):
-    // beside the producer every KiB of LDS per wave is consensus residency
-    const bool pg = a.pts_global && B.xy;
-    const double2 *P = pg ? (const double2 *)B.xy + p0 : Ps;
 #ifdef LSLAM_STAMPS
     unsigned long long *chdbg = a.dbg ? a.dbg + (size_t)c * 16 : nullptr;
 #else
@@ -2270,23 +2265,22 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     } else {
         const int32_t *h = (HYP == LSLAM_HYP_EXPLICIT ? B.hyp : a.draws_scr) + (size_t)c * 2 * D;
         dr = h;
-        if (pg) {
-        } else if (N <= 128 && B.xy) {
+        if (N <= 128 && B.xy) {
             double2 pv[2];
             const double2 *src = (const double2 *)B.xy + p0;
 #pragma unroll
             for (int k = 0; k < 2; k++) pv[k] = (lane + 64 * k < N) ? src[lane + 64 * k] : make_double2(0.0, 0.0);
 #pragma unroll
             for (int k = 0; k < 2; k++)
-                if (lane + 64 * k < N) Ps[lane + 64 * k] = pv[k];
+                if (lane + 64 * k < N) P[lane + 64 * k] = pv[k];
         } else {
-            stage_points(B, p0, N, Ps, lane);
+            stage_points(B, p0, N, P, lane);
         }
         if (HYP == LSLAM_HYP_EXPLICIT && B.draws_out)
             for (int i = lane; i < 2 * D; i += 64) B.draws_out[(size_t)c * 2 * D + i] = h[i];
     }
     CH_STAMP(0);
-    if (HYP == LSLAM_HYP_PHILOX && !pg) stage_points(B, p0, N, Ps, lane);
+    if (HYP == LSLAM_HYP_PHILOX) stage_points(B, p0, N, P, lane);
     __syncthreads();
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
@@ -3509,7 +3503,7 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
     const int T = k.T;
     int off = 0;
-    k.off_pts = off; off += k.pts_global ? 0 : align16(16 * N);
+    k.off_pts = off; off += align16(16 * N);
     k.off_draws = off; off += (k.hyp_source == LSLAM_HYP_PHILOX) ? align16(8 * (T + 1)) : 0;  // else read in place
     k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
@@ -3944,8 +3938,6 @@ static int launch_chunks(lslam_ctx *c, const KArgs &base, bool write_yproj) {
         return timer_end(c, LSLAM_K_CONSENSUS);
     }
     int lds = 0;
-    static const bool gpts = [] { const char *e = getenv("LSLAM_CHUNK_GPTS"); return e && atoi(e) != 0; }();
-    k.pts_global = (gpts && k.b.xy) ? 1 : 0;
     st = layout_chunk(k, &k.b, lds);
     if (st) return st;
     static std::once_flag once;
