@@ -3,21 +3,23 @@
 // points each function replaces and DESIGN.md for the layout/roofline notes.
 //
 // Execution model (lslam_scan_pipeline, parity mode):
-//   rng_kernel     (producer stream) one parser wave per scan, 4 parsers + 1
-//                  twisting helper per workgroup: the scan's chained legacy
+//   rng_kernel     (producer stream) one parser wave per scan, 4 parsers per
+//                  workgroup, each twisting its own MT blocks: the scan's chained legacy
 //                  MT19937 stream (ransac_functions.py:73 + fit.py:791) -> the
 //                  j of every Fisher-Yates step, assuming no early stop
 //                  (lslam_rng_pipe.h)
-//   resolve_kernel one wave per chunk (resolve_big_kernel: per 64 draws when the
-//                  chunk's steps exceed the LDS stage): steps -> the T+1 draws
+//   resolve_reg8_kernel one wave per (chunk, 64 draws) (resolve_kernel / _walk /
+//                  _big for other sizes and epochs): steps -> the T+1 draws
 //   chunk_kernel   one wave per chunk: A4/A5 counts (lane = hypothesis), A6 tie
 //                  sums + selection, mask + A7 refit, A8 line parameters
 //                  (chunks of > 128 points: model / count / select kernels)
 //   scan_kernel    (fix-up) one wave per scan; exits at once unless one of its
 //                  chunks stopped early, then replays the scan sequentially
+//   ukf_group_kernel U1-U8 on lane groups (16 lanes per scan at L = 20), 4-wave
+//                  workgroups, between the fix-up and the post pass
 //   scan_kernel    (post) one wave per scan: A9/A10 association walk over the
-//                  chunks in order, y_proj, then U1-U8 UKF (LSLAM_UKF_MAP:
-//                  predict, world-frame association, update with the matches)
+//                  chunks in order (list in registers up to 64 landmarks), y_proj
+//                  (LSLAM_UKF_MAP: predict, world-frame association, update)
 // Philox / explicit hypotheses skip the producer and the fix-up.  A chunk's
 // points, draws and scratch live in LDS; HBM sees the points once per pass.
 //
@@ -1546,13 +1548,13 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
 
 // ------------------------------------------------------------------------
 // rng_kernel: the chained parity stream of one scan -> every chunk's draws
-// (wave 0 parses, wave 1 twists ahead and resolves; lslam_rng_pipe.h)
+// (lslam_rng_pipe.h)
 // ------------------------------------------------------------------------
-// PPW parser waves (one scan each) + one helper wave per workgroup.  One helper
-// twists for all PPW parsers (it is asleep most of the time), so a 4096-scan
-// batch holds 5 waves per SIMD instead of 8: the producer no longer needs every
-// wave slot of the chip, and the previous call's consumers run beside it
-// without holding back any of its workgroups.
+// PPW parser waves (one scan each) per workgroup.  Launched with 64 * PPW threads (the
+// default) each parser twists its own blocks; launched with 64 * (PPW + 1) (LSLAM_RNG_SELF=0)
+// the last wave is a helper that twists for all PPW parsers (asleep most of the time).  A
+// 4096-scan batch then holds 4 (or 5) waves per SIMD: the previous call's consumers run
+// beside it in the other slots.
 template <typename JT, int PPW>
 __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -12,11 +12,14 @@
 //                     J[c][d][s] = j of step s (i = K - s) of draw d of chunk c,
 //                     at D * chunk_pt_off[c] + d*K + s (u8 if every chunk has
 //                     <= 256 points, else u16).
-//   wave 1 (helper):  twists block b+1 of the MT state out of place while the
-//                     parser reads block b (two 624-word slots of raw state,
-//                     then a 64-word pad holding slot 0's head, so a window
-//                     may run across the block boundary).  It sleeps until a
-//                     parser wakes it (s_wakeup) at a block switch (rng_kernel).
+//   blocks:           block b+1 of the MT state is twisted out of place into the
+//                     other of two 624-word slots of raw state (then a 64-word
+//                     pad holding slot 0's head, so a window may run across the
+//                     block boundary).  By default the parser twists it itself
+//                     when it first needs it (rp_need_block: one producer wave
+//                     per SIMD fewer beside the consumers); with
+//                     LSLAM_RNG_SELF=0 a helper wave per workgroup twists ahead
+//                     and sleeps until a parser's s_wakeup (rng_kernel).
 // Turning the steps into the two drawn indices is bulk, data-parallel work
 // (resolve_chunk below); it runs in the consensus kernel, one wave per chunk,
 // where all of a chunk's draws are resolved together.
