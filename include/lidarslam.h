@@ -30,6 +30,8 @@
  *   lslam_ukf_step        systemClass.py:12-29 System.ukf.predict(u=..) +
  *                         .update(z, landmarks=..) with UKFMethods.py:10-71
  *                         callbacks (filterpy 1.4.5 UnscentedKalmanFilter semantics)
+ *   lslam_ukf_trace       the same, exposing UKFMethods.py:26-34 hx and :60-71
+ *                         residuals for the reference-pinned tests
  */
 #ifndef LIDARSLAM_H
 #define LIDARSLAM_H
@@ -41,7 +43,7 @@
 extern "C" {
 #endif
 
-#define LSLAM_ABI_VERSION 3
+#define LSLAM_ABI_VERSION 4
 
 /* ---- status codes ---- */
 enum {
@@ -92,7 +94,12 @@ enum {
      * models[c] keeps the robot-frame fit; proj_a/proj_b (y_proj) stay the chunk's own line.
      * id_base (if given) is in/out in this mode: advanced by the scan's chunk count, as
      * check_ransac's landmarkNumber (ransac_functions.py:77), so steps chain without host syncs. */
-    LSLAM_UKF_MAP = 8
+    LSLAM_UKF_MAP = 8,
+    /* lslam_ukf_step, an UPDATE without PREDICT in the same call: the sigma points are read from
+     * lslam_scan_batch.ukf_sigmas (filterpy's self.sigmas_f, cached by the last predict) instead of
+     * being drawn from (x, P); x and P are the current ones (filterpy UKF.update: cross_variance(self.x,
+     * zp, self.sigmas_f, ...), self.P - K S K^T).  Not supported by lslam_scan_pipeline. */
+    LSLAM_UKF_SIGMAS_IN = 16
 };
 
 /* One RANSAC call's result (one chunk), 112 bytes. */
@@ -185,6 +192,10 @@ typedef struct lslam_scan_batch {
      * x = d cos(-th * pi/180 + pi/2), y = d sin(...), bit-identical to lslam_polar_to_xy. */
     const double *theta_deg;        /* [n_points] */
     const double *dist_mm;          /* [n_points] */
+    /* ABI 4: filterpy's sigmas_f per scan, [n_scans][7][3] (optional; lslam_ukf_step only): a PREDICT
+     * writes the sigma points re-drawn from the predicted (x, P); an UPDATE with LSLAM_UKF_SIGMAS_IN
+     * reads them.  NULL: not written, and an update draws its sigma points from (x, P). */
+    double *ukf_sigmas;
 } lslam_scan_batch;
 
 /* Express-scan measures (lslam_express_decode): device arrays, NULL = not written.
@@ -291,6 +302,16 @@ int lslam_ransac(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_p
 int lslam_landmarks(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ransac_params *p);
 /* U1-U8: one predict and/or update per scan */
 int lslam_ukf_step(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ukf_params *u);
+/* Test / diagnostic: lslam_ukf_step (the same kernel code, lane-group form) that also writes the
+ * update's intermediate values per scan to trace (device, [n_scans][42 + 32 L] doubles, m = 2L):
+ *   [0, 21)            sigma points sigma_k (k = 0..6, [x, y, theta])
+ *   [21, 42)           residual_x(sigma_k, x)                           UKFMethods.py:60-63
+ *   [42, 42 + 7m)      hx(sigma_k) = transfer_function(sigma_k, lmk)    UKFMethods.py:26-34
+ *   [42 + 7m, +m)      zp (z_mean about sigma 0)
+ *   [42 + 8m, +m)      residual_h(z, zp)                                UKFMethods.py:66-71
+ *   [42 + 9m, +7m)     residual_h(hx(sigma_k), zp)
+ * Entries of inactive landmark slots are not written.  Needs LSLAM_UKF_UPDATE; not in MAP mode. */
+int lslam_ukf_trace(lslam_ctx *ctx, const lslam_scan_batch *b, const lslam_ukf_params *u, double *trace);
 /* A3-A10 (+ U1-U8 if u != NULL) for every scan of the batch in one call: MT19937 producer (its
  * own stream, overlapping the previous call's consumers), resolve, consensus, fix-up, then the
  * association / UKF post pass */

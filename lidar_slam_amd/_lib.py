@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSLAM_LIB") or os.path.join(_HERE, "liblidarslam.so")  # override: experiments
 
 # ---- constants mirrored from include/lidarslam.h ----
-ABI_VERSION = 3  # include/lidarslam.h LSLAM_ABI_VERSION (struct layouts below)
+ABI_VERSION = 4  # include/lidarslam.h LSLAM_ABI_VERSION (struct layouts below)
 LSLAM_OK = 0
 LSLAM_ERR_ARG = -1
 LSLAM_ERR_HIP = -2
@@ -27,7 +27,7 @@ EARLY_STOP, VERTICAL, NEW_LANDMARK, MATCHED = 16, 32, 64, 128
 CAPACITY = 256
 
 HYP_MT19937, HYP_PHILOX, HYP_EXPLICIT = 0, 1, 2
-UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC, UKF_MAP = 1, 2, 4, 8
+UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC, UKF_MAP, UKF_SIGMAS_IN = 1, 2, 4, 8, 16
 K_POLAR, K_HYP, K_PIPELINE, K_LANDMARK, K_UKF, K_RNG, K_CONSENSUS = 0, 1, 2, 3, 4, 5, 6
 K_EXPRESS, K_EXPRESS_SCATTER = 7, 8
 
@@ -70,7 +70,7 @@ class ScanBatch(C.Structure):
                [(n, _VP) for n in ("xy", "scan_chunk_off", "chunk_pt_off", "seeds", "mt_state_in", "mt_state_out",
                                    "hyp", "id_base", "landmarks", "lmk_count", "lmk_walk", "inlier_mask", "models", "y_proj",
                                    "draws_out", "trial_cnt_out", "ukf_x", "ukf_P", "ukf_u", "ukf_z", "ukf_lmk",
-                                   "ukf_R_diag", "theta_deg", "dist_mm")]
+                                   "ukf_R_diag", "theta_deg", "dist_mm", "ukf_sigmas")]
 
 
 class ExpressMeasures(C.Structure):
@@ -93,7 +93,7 @@ EXPORTS = [
     "lslam_timing_reset", "lslam_set_steps_budget",
     "lslam_ransac_params_default", "lslam_ukf_params_default", "lslam_inlier_cutoff", "lslam_ukf_weights",
     "lslam_mt_seed_state", "lslam_polar_to_xy", "lslam_hyp_mt19937", "lslam_ransac", "lslam_landmarks",
-    "lslam_ukf_step", "lslam_scan_pipeline", "lslam_express_decode", "lslam_express_scans",
+    "lslam_ukf_step", "lslam_ukf_trace", "lslam_scan_pipeline", "lslam_express_decode", "lslam_express_scans",
 ]
 
 _lib = None
@@ -153,6 +153,7 @@ def load():
         "lslam_ransac": ([_VP, P(ScanBatch), P(RansacParams)], C.c_int),
         "lslam_landmarks": ([_VP, P(ScanBatch), P(RansacParams)], C.c_int),
         "lslam_ukf_step": ([_VP, P(ScanBatch), P(UkfParams)], C.c_int),
+        "lslam_ukf_trace": ([_VP, P(ScanBatch), P(UkfParams), _VP], C.c_int),
         "lslam_scan_pipeline": ([_VP, P(ScanBatch), P(RansacParams), P(UkfParams)], C.c_int),
         "lslam_express_decode": ([_VP, _VP, i64, P(ExpressMeasures)], C.c_int),
         "lslam_express_scans": ([_VP, _VP, i64, i32, P(ExpressRevs)], C.c_int),

@@ -1493,7 +1493,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void sc
 // UKF step of the fused pipeline on groups of Pg lanes per scan (lslam_ukf.h: ukf_step_group),
 // after the association pass; the landmark slots [0, nchunks) take the scan's fitted chunk
 // origins (LMK_FROM_RANSAC) exactly as the post pass's corg does (models with LSLAM_VALID)
-__global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, int fuse) {
+// VAR != 0 (lslam_ukf_step's sigma cache / lslam_ukf_trace, lslam_ukf.h UKF_VAR_*) instantiates the same
+// step with those extra loads and stores; the pipeline's launches are VAR = 0.
+template <int VAR>
+__global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, int fuse, double *trace) {
     const lslam_scan_batch &B = a.b;
     const int lane = (int)threadIdx.x & 63;
     const int g = lane & (Pg - 1);
@@ -1524,7 +1527,10 @@ __global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, i
         }
         return true;
     };
-    ukf_step_group(x, Pm, u0, u1, B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, a.ukf.flags, g, Pg);
+    double *sio = (VAR & UKF_VAR_SIGMAS) ? B.ukf_sigmas + (size_t)s * 21 : nullptr;
+    double *tr = (VAR & UKF_VAR_TRACE) ? trace + (size_t)s * ukf_tr_doubles(Lu) : nullptr;
+    ukf_step_group<VAR>(x, Pm, u0, u1, B.ukf_z + (size_t)s * 2 * Lu, B.ukf_R_diag, lmk_fn, a.ukf, a.ukf.flags, g, Pg,
+                        sio, tr);
     if (g == 0) {
         for (int i = 0; i < 3; i++) B.ukf_x[3 * (size_t)s + i] = x[i];
         for (int i = 0; i < 9; i++) B.ukf_P[9 * (size_t)s + i] = Pm[i];
@@ -1533,7 +1539,7 @@ __global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, i
 
 // lanes per scan: about two landmarks per lane, up to a wave (C3: 16 lanes, 4 scans per wave,
 // one round of waves beside the producer; one landmark per lane: +1 % per C3 step, five: +2 %)
-static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream, bool fuse) {
+static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream, bool fuse, double *trace = nullptr) {
     int Pg = 1;
     while (Pg < (n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
     const int per = 64 / Pg;
@@ -1542,8 +1548,14 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
     // stack two on some SIMDs (full register file) and hold the next producer off that CU
     static const int wpg = [] { const char *e = getenv("LSLAM_UKF_WG"); const int v = e ? atoi(e) : 4; return v >= 1 && v <= 4 ? v : 4; }();
     const int nwaves = (k.b.n_scans + per - 1) / per;
-    hipLaunchKernelGGL(ukf_group_kernel, dim3((unsigned)((nwaves + wpg - 1) / wpg)), dim3(64 * wpg), 0, stream, k, Pg,
-                       fuse ? 1 : 0);
+    const dim3 grid((unsigned)((nwaves + wpg - 1) / wpg)), block(64 * wpg);
+    const int var = (trace ? UKF_VAR_TRACE : 0) | (k.b.ukf_sigmas ? UKF_VAR_SIGMAS : 0);
+    switch (fuse ? 0 : var) {
+        case 0: hipLaunchKernelGGL(ukf_group_kernel<0>, grid, block, 0, stream, k, Pg, fuse ? 1 : 0, nullptr); break;
+        case 1: hipLaunchKernelGGL(ukf_group_kernel<1>, grid, block, 0, stream, k, Pg, 0, trace); break;
+        case 2: hipLaunchKernelGGL(ukf_group_kernel<2>, grid, block, 0, stream, k, Pg, 0, nullptr); break;
+        default: hipLaunchKernelGGL(ukf_group_kernel<3>, grid, block, 0, stream, k, Pg, 0, trace); break;
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -4281,7 +4293,7 @@ int lslam_landmarks(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_
     return end_call(c);
 }
 
-int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u) {
+static int ukf_step_impl(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u, double *trace) {
     if (!c || !u || !b) return LSLAM_ERR_ARG;
     if (b->n_scans < 0) return LSLAM_ERR_ARG;
     lslam_scan_batch bb = *b;
@@ -4291,10 +4303,37 @@ int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_para
     if (!bb.scan_chunk_off) return set_err(LSLAM_ERR_ARG, "scan_chunk_off required (may describe 0 chunks)");
     int st = build_args(k, &bb, nullptr, u, MODE_UKF, lds);
     if (st) return st;
-    if ((st = run_scan_kernel<MODE_UKF>(c, k, lds, LSLAM_K_UKF))) return st;
+    const bool lanes = c->ukf_lanes && !(u->flags & LSLAM_UKF_MAP);
+    if ((u->flags & LSLAM_UKF_SIGMAS_IN) && !b->ukf_sigmas)
+        return set_err(LSLAM_ERR_ARG, "LSLAM_UKF_SIGMAS_IN without ukf_sigmas");
+    if ((b->ukf_sigmas || trace) && !lanes)
+        return set_err(LSLAM_ERR_UNSUPPORTED, "ukf_sigmas / trace need the lane-group UKF (not MAP, LSLAM_UKF_LANES != 0)");
+    if (trace && !(u->flags & LSLAM_UKF_UPDATE)) return set_err(LSLAM_ERR_ARG, "lslam_ukf_trace needs LSLAM_UKF_UPDATE");
+    if (trace || b->ukf_sigmas) {
+        HIPCHK(hipSetDevice(c->device));
+        if (k.b.n_scans > 0) {
+            if ((st = timer_begin(c, LSLAM_K_UKF))) return st;
+            launch_ukf_group(k, k.ukf.L, c->stream, false, trace);
+            HIPCHK(hipGetLastError());
+            if ((st = timer_end(c, LSLAM_K_UKF))) return st;
+        }
+    } else if ((st = run_scan_kernel<MODE_UKF>(c, k, lds, LSLAM_K_UKF))) {
+        return st;
+    }
     note_out(c, b->ukf_x, (size_t)b->n_scans * 24);
     note_out(c, b->ukf_P, (size_t)b->n_scans * 72);
+    if (b->ukf_sigmas) note_out(c, b->ukf_sigmas, (size_t)b->n_scans * 168);
+    if (trace) note_out(c, trace, (size_t)b->n_scans * 8 * ukf_tr_doubles(u->n_landmarks));
     return end_call(c);
+}
+
+int lslam_ukf_step(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u) {
+    return ukf_step_impl(c, b, u, nullptr);
+}
+
+int lslam_ukf_trace(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ukf_params *u, double *trace) {
+    if (!trace) return set_err(LSLAM_ERR_ARG, "trace buffer required");
+    return ukf_step_impl(c, b, u, trace);
 }
 
 int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac_params *p,
@@ -4302,6 +4341,8 @@ int lslam_scan_pipeline(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ran
     if (!c || !p) return LSLAM_ERR_ARG;
     int st = validate_batch(b, true);
     if (st) return st;
+    if (u && ((u->flags & LSLAM_UKF_SIGMAS_IN) || b->ukf_sigmas))
+        return set_err(LSLAM_ERR_UNSUPPORTED, "ukf_sigmas / LSLAM_UKF_SIGMAS_IN are lslam_ukf_step's (filterpy's cache)");
     return run_split(c, b, p, u);
 }
 

@@ -432,9 +432,28 @@ __device__ bool ukf_step(double x[3], double P[9], double u0, double u1, const d
 // the sigma order k = 0..6; M X = [b | Dx] is solved directly (Gauss-Jordan, partial pivoting)
 // instead of forming M^-1, so the last bits differ from ukf_step; both are held to the 50-digit
 // evaluation per component (tests/test_gpu_ukf_exact.py).
-template <typename LmkFn>
+//
+// VAR (lslam_ukf_step only; the pipeline's kernels run VAR = 0): bit UKF_VAR_SIGMAS reads and
+// writes filterpy's cached sigma points through `sio` ([7][3], the scan's ukf_sigmas): a predict
+// stores the re-drawn sigmas_f there, and an update without a predict in the same call
+// (LSLAM_UKF_SIGMAS_IN) takes them from there instead of drawing them from (x, P), as
+// filterpy's update uses self.sigmas_f with the current self.x and self.P.  Bit UKF_VAR_TRACE
+// writes the step's intermediate values to `tr` (layout UKF_TR_*; the lane that owns a
+// landmark writes its entries), so tests can read hx and the wrapped residuals.
+enum { UKF_VAR_TRACE = 1, UKF_VAR_SIGMAS = 2 };
+__host__ __device__ constexpr int ukf_tr_doubles(int L) { return 42 + 16 * 2 * L; }
+// per-scan trace layout (doubles, m = 2L): update's sigma points [7][3], Dx = residual_x(sigma_k, x)
+// [7][3], hx(sigma_k) [7][m], zp [m], y = residual_h(z, zp) [m], rz_k = residual_h(hx(sigma_k), zp) [7][m]
+__host__ __device__ constexpr int ukf_tr_hx(int L) { return 42; }
+__host__ __device__ constexpr int ukf_tr_zp(int L) { return 42 + 7 * 2 * L; }
+__host__ __device__ constexpr int ukf_tr_yr(int L) { return 42 + 8 * 2 * L; }
+__host__ __device__ constexpr int ukf_tr_rz(int L) { return 42 + 9 * 2 * L; }
+
+template <int VAR = 0, typename LmkFn>
 __device__ bool ukf_step_group(double x[3], double P[9], double u0, double u1, const double *z, const double *Rd,
-                               LmkFn lmk, const UkfConst &C, int flags, int g, int Pg) {
+                               LmkFn lmk, const UkfConst &C, int flags, int g, int Pg, double *sio = nullptr,
+                               double *tr = nullptr) {
+    constexpr bool kTrace = (VAR & UKF_VAR_TRACE) != 0, kSig = (VAR & UKF_VAR_SIGMAS) != 0;
     bool ok = true;
     double U[9];
     double sig[21];
@@ -480,8 +499,9 @@ __device__ bool ukf_step_group(double x[3], double P[9], double u0, double u1, c
         x[1] = xm1;
         x[2] = xm2;
     }
-    if (!(flags & 2)) return ok;
-    {
+    const bool sig_in = kSig && !(flags & 1) && (flags & LSLAM_UKF_SIGMAS_IN);
+    if (!(flags & 2) && !(kSig && (flags & 1))) return ok;
+    if (!sig_in) {
         double A[9];
 #pragma unroll
         for (int i = 0; i < 9; i++) A[i] = C.cfac * P[i];
@@ -491,10 +511,28 @@ __device__ bool ukf_step_group(double x[3], double P[9], double u0, double u1, c
     double Dx[21];
 #pragma unroll
     for (int k = 0; k < 7; k++) {
-        sigma_point(k, x, U, sig + 3 * k);
+        if (sig_in) {
+            sig[3 * k] = sio[3 * k];
+            sig[3 * k + 1] = sio[3 * k + 1];
+            sig[3 * k + 2] = sio[3 * k + 2];
+        } else {
+            sigma_point(k, x, U, sig + 3 * k);
+        }
         Dx[3 * k] = sig[3 * k] - x[0];
         Dx[3 * k + 1] = sig[3 * k + 1] - x[1];
         Dx[3 * k + 2] = wrap_angle(sig[3 * k + 2] - x[2]);
+    }
+    if constexpr (kSig) {
+        if ((flags & 1) && g == 0)
+            for (int e = 0; e < 21; e++) sio[e] = sig[e];  // filterpy's sigmas_f after predict
+        if (!(flags & 2)) return ok;
+    }
+    if constexpr (kTrace) {
+        if (g == 0)
+            for (int e = 0; e < 21; e++) {
+                tr[e] = sig[e];
+                tr[21 + e] = Dx[e];
+            }
     }
     // G = Y R^-1 Y^T (upper triangle, row-major k <= l) and b = Y R^-1 y over the landmarks
     double G[28], bv[7];
@@ -531,6 +569,19 @@ __device__ bool ukf_step_group(double x[3], double P[9], double u0, double u1, c
         for (int k = 0; k < 7; k++) {
             r0[k] = d[k] - dm;
             r1[k] = wrap_angle(ph[k] - pm);
+        }
+        if constexpr (kTrace) {
+            const int m = 2 * C.L;
+            for (int k = 0; k < 7; k++) {
+                tr[ukf_tr_hx(C.L) + k * m + 2 * j] = d[k];
+                tr[ukf_tr_hx(C.L) + k * m + 2 * j + 1] = ph[k];
+                tr[ukf_tr_rz(C.L) + k * m + 2 * j] = r0[k];
+                tr[ukf_tr_rz(C.L) + k * m + 2 * j + 1] = r1[k];
+            }
+            tr[ukf_tr_zp(C.L) + 2 * j] = dm;
+            tr[ukf_tr_zp(C.L) + 2 * j + 1] = pm;
+            tr[ukf_tr_yr(C.L) + 2 * j] = yr0;
+            tr[ukf_tr_yr(C.L) + 2 * j + 1] = yr1;
         }
         int e = 0;
 #pragma unroll

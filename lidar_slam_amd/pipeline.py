@@ -213,6 +213,21 @@ class ScanPipeline:
         if sync:
             self.ctx.sync()
 
+    def run_ukf_trace(self):
+        """lslam_ukf_trace (a test/diagnostic form of run_ukf_only): the step's intermediate values
+        per scan, as a dict of arrays (include/lidarslam.h: sigma points, residual_x, hx(sigma_k),
+        zp, residual_h(z, zp), residual_h(hx(sigma_k), zp))."""
+        L = int(self.up.n_landmarks)
+        m, n = 2 * L, 42 + 32 * L
+        tr = self.ctx.empty((max(self.S, 1), n), np.float64)
+        tr.upload(np.full((max(self.S, 1), n), np.nan))   # inactive slots stay NaN
+        _lib.check(_lib.load().lslam_ukf_trace(self.ctx.handle, C.byref(self.batch), C.byref(self.up), tr.ptr),
+                   "lslam_ukf_trace")
+        t = tr.download()[:self.S]
+        return {"sigmas": t[:, :21].reshape(-1, 7, 3), "dx": t[:, 21:42].reshape(-1, 7, 3),
+                "hx": t[:, 42:42 + 7 * m].reshape(-1, 7, m), "zp": t[:, 42 + 7 * m:42 + 8 * m],
+                "y": t[:, 42 + 8 * m:42 + 9 * m], "rz": t[:, 42 + 9 * m:].reshape(-1, 7, m)}
+
     def results(self):
         out = {"mask": self.mask.download()[:self.P], "models": self.models.download()[:self.C]}
         if hasattr(self, "yproj"):

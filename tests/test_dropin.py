@@ -175,3 +175,80 @@ def test_revolution_dispatcher_thread_and_error_replay():
     # a 2-point chunk raises ValueError at that chunk, as in the reference
     with pytest.raises(ValueError):
         ransac_functions.process_revolution([line(50, 1.0), line(2, 1.0)], 0, [])
+
+
+def test_ukf_dropin_arguments_are_strict():
+    """filterpy's call surface (systemClass.py:21-29): per-call dt / R, required u / landmarks,
+    and what the GPU step cannot represent raises instead of being dropped (CPU: the argument
+    handling of lidar_slam_amd/ukf.py, no device)."""
+    from lidar_slam_amd import ukf
+    u, dt = ukf.predict_args(None, None, None, {"u": [2.0, 2.5]}, 0.005)
+    assert dt == 0.005 and np.array_equal(u, [2.0, 2.5])
+    assert ukf.predict_args(0.01, None, None, {"u": (0, 0)}, 0.005)[1] == 0.01
+    with pytest.raises(TypeError):
+        ukf.predict_args(None, None, None, {}, 0.005)           # transition_function needs u
+    with pytest.raises(TypeError):
+        ukf.predict_args(None, None, None, {"u": (0, 0), "v": 1}, 0.005)
+    with pytest.raises(ValueError):
+        ukf.predict_args(None, None, lambda *a: a, {"u": (0, 0)}, 0.005)
+    R = np.diag([0.25, 0.09] * 2)
+    lm = [(1.0, 2.0), (3.0, 4.0)]
+    Rd, pos = ukf.update_args(None, None, None, {"landmarks": lm}, R, 4)
+    assert np.array_equal(Rd, [0.25, 0.09] * 2) and np.array_equal(pos, [1.0, 2.0, 3.0, 4.0])
+    Rd, _ = ukf.update_args(2.0, None, None, {"landmarks": lm}, R, 4)    # scalar R: eye * R, this call only
+    assert np.array_equal(Rd, [2.0] * 4)
+    Rn = R.copy()
+    Rn[0, 1] = Rn[1, 0] = 0.01
+    with pytest.raises(ValueError, match="diagonal"):
+        ukf.update_args(None, None, None, {"landmarks": lm}, Rn, 4)       # non-diagonal R is not dropped
+    with pytest.raises(ValueError):
+        ukf.update_args(np.eye(3), None, None, {"landmarks": lm}, R, 4)
+    with pytest.raises(TypeError):
+        ukf.update_args(None, None, None, {}, R, 4)                       # transfer_function needs landmarks
+    with pytest.raises(ValueError):
+        ukf.update_args(None, None, None, {"landmarks": lm[:1]}, R, 4)
+    from lidar_slam_amd import landmarking as lmk
+    L = lmk.Landmark(0.5, 3.0, 7, 10.0, 20.0, 50.0, 28.0)
+    _, pos = ukf.update_args(None, None, None, {"landmarks": [L, L]}, R, 4)   # Landmark.get_pos()
+    assert np.array_equal(pos, [10.0, 20.0, 10.0, 20.0])
+
+
+@pytest.mark.gpu
+def test_system_ukf_keeps_filterpy_state():
+    """filterpy keeps sigmas_f from predict: update uses them with the CURRENT x and P, so
+    predict -> set x -> update, update twice, and update before any predict (sigmas_f = 0)
+    follow oracle/ukf.py's UKF (the same state handling) to 1e-5 per component."""
+    from oracle import ukf as oukf
+    from oracle import ukf_exact
+    rng = np.random.default_rng(7)
+    lm = [tuple(p) for p in rng.uniform(-3000, 3000, (8, 2))]
+    x0 = np.array([1000.0, 800.0, 0.3])
+    z = oukf.transfer_function(x0, lm) + rng.normal(0, 0.2, 16)
+
+    def both():
+        sysm = systemClass.System([])
+        f = oukf.UKF(8)
+        sysm.ukf.x, f.x = x0.copy(), x0.copy()
+        return sysm.ukf, f
+
+    def close(g, f):
+        err = ukf_exact.component_errors(g.x[None], g.P[None], f.x[None], f.P[None])
+        assert max(err.values()) <= 1e-5, err
+
+    g, f = both()                                   # predict -> set x -> update
+    g.predict(u=[2.0, 2.5])
+    f.predict(np.array([2.0, 2.5]))
+    assert np.allclose(g.sigmas_f, f.sigmas_f, rtol=1e-9, atol=1e-9)
+    g.x = f.x = f.x + np.array([3.0, -2.0, 0.01])
+    g.update(z, landmarks=lm)
+    f.update(z, lm)
+    close(g, f)
+    g.update(z, landmarks=lm)                       # a second update reuses the same sigmas_f
+    f.update(z, lm)
+    close(g, f)
+    g, f = both()                                   # update first: filterpy's zero sigmas_f
+    assert not np.any(g.sigmas_f)
+    g.P = f.P = np.diag([4.0, 4.0, 0.01])
+    g.update(z, landmarks=lm)
+    f.update(z, lm)
+    assert np.all(np.isfinite(g.x)) and np.allclose(g.x, f.x, rtol=1e-6, atol=1e-6)
