@@ -24,7 +24,7 @@ LSLAM_ERR_UNSUPPORTED = -5
 
 VALID, N_TOO_SMALL, NO_INLIERS, EST_FAIL = 1, 2, 4, 8
 EARLY_STOP, VERTICAL, NEW_LANDMARK, MATCHED = 16, 32, 64, 128
-CAPACITY = 256
+CAPACITY, CHUNK_BOUND = 256, 512
 
 HYP_MT19937, HYP_PHILOX, HYP_EXPLICIT = 0, 1, 2
 UKF_PREDICT, UKF_UPDATE, UKF_LMK_FROM_RANSAC, UKF_MAP, UKF_SIGMAS_IN = 1, 2, 4, 8, 16

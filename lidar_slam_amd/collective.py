@@ -105,6 +105,29 @@ def _addr(x, off=0):
     return C.c_void_p(base + int(off))
 
 
+def gatherv_plan(rank, world, counts, root=0):
+    """This rank's share of ``gatherv`` as (kind, peer, offset, nbytes) operations, in issue order:
+
+    * on the root: ("copy", root, off_root, n) for its own bytes (send[0:n] -> recv[off:off+n]),
+      then ("recv", r, off_r, n_r) for every other rank r with n_r > 0, where
+      off_r = sum(counts[:r]);
+    * elsewhere: ("send", root, 0, n) of send[0:n], if n = counts[rank] > 0.
+    Zero-count ranks issue nothing and are expected by nobody.  The RCCL transport runs the
+    send/recv ops inside one ncclGroupStart/End (lidar_slam_amd/collective.py Comm.gatherv); the
+    CPU tests run the same plan over gloo (tests/test_shard.py)."""
+    world, rank, root = int(world), int(rank), int(root)
+    counts = [int(n) for n in counts]
+    if len(counts) != world or min(counts, default=0) < 0 or not (0 <= root < world) or not (0 <= rank < world):
+        raise ValueError("gatherv: need world = len(counts), counts >= 0 and ranks in [0, world)")
+    offs = [0]
+    for n in counts:
+        offs.append(offs[-1] + n)
+    if rank != root:
+        return [("send", root, 0, counts[rank])] if counts[rank] else []
+    ops = [("copy", root, offs[root], counts[root])] if counts[root] else []
+    return ops + [("recv", r, offs[r], counts[r]) for r in range(world) if r != root and counts[r]]
+
+
 class Comm:
     """One rank of an RCCL communicator bound to an lslam context (its device and stream)."""
 
@@ -133,26 +156,26 @@ class Comm:
 
     def gatherv(self, send, recv, counts, root=0):
         """Rank r's first counts[r] bytes of ``send`` -> ``recv`` at sum(counts[:r]) on root."""
+        ops = gatherv_plan(self.rank, self.world, counts, root)
         L = load()
-        offs = [0]
-        for n in counts:
-            offs.append(offs[-1] + int(n))
         st = self._stream
-        if self.rank == root and counts[root]:
-            self.ctx.copy(_addr(recv, offs[root]).value, _addr(send).value, counts[root])
-        if self.world == 1:
+        p2p = [op for op in ops if op[0] != "copy"]
+        for kind, _, off, n in ops:
+            if kind == "copy":
+                self.ctx.copy(_addr(recv, off).value, _addr(send).value, n)
+        if not p2p:
             return
         _check(L.ncclGroupStart(), "ncclGroupStart")
         try:
-            if self.rank == root:
-                for r in range(self.world):
-                    if r != root and counts[r]:
-                        _check(L.ncclRecv(_addr(recv, offs[r]), int(counts[r]), NCCL_UINT8, r, self._comm, st),
-                               "ncclRecv")
-            elif counts[self.rank]:
-                _check(L.ncclSend(_addr(send), int(counts[self.rank]), NCCL_UINT8, root, self._comm, st), "ncclSend")
-        finally:
-            _check(L.ncclGroupEnd(), "ncclGroupEnd")
+            for kind, peer, off, n in p2p:
+                if kind == "recv":
+                    _check(L.ncclRecv(_addr(recv, off), n, NCCL_UINT8, peer, self._comm, st), "ncclRecv")
+                else:
+                    _check(L.ncclSend(_addr(send, off), n, NCCL_UINT8, peer, self._comm, st), "ncclSend")
+        except BaseException:
+            L.ncclGroupEnd()  # close the group; the body's error is the one reported
+            raise
+        _check(L.ncclGroupEnd(), "ncclGroupEnd")
 
     def broadcast(self, buf, nbytes, root=0):
         """In-place broadcast of ``nbytes`` of a device buffer from ``root``."""
@@ -181,4 +204,4 @@ def available() -> bool:
         return False
 
 
-__all__ = ["Comm", "RcclError", "available", "load", "unique_id", "version"]
+__all__ = ["Comm", "RcclError", "available", "gatherv_plan", "load", "unique_id", "version"]

@@ -1199,8 +1199,17 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 
     if (use_mt) mt_init();
 
+    // the staged post passes hold the scan's chunk records in an LDS area of max_scan_chunks
+    // (hist_cap) records: a scan with more chunks than the batch declared takes the per-chunk
+    // loop below, or, with the register list (which has no LDS list to fall back on), is
+    // flagged LSLAM_CHUNK_BOUND and left unassociated
+    const bool recs_fit = nchunks <= a.hist_cap;
     if constexpr (kPost && (MODE & MODE_ASSOC) != 0 && (MODE & MODE_UKF) == 0) {
         if (a.lmk_reg) {  // the list in registers (association-only post pass, lmk_cap <= 64)
+            if (!recs_fit) {
+                for (int c = c0 + lane; c < c1; c += 64) B.models[c].flags |= LSLAM_CHUNK_BOUND;
+                return;
+            }
             post_assoc_reg(a, s, smem + a.off_recs, lane);
             return;
         }
@@ -1242,7 +1251,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
 
     bool chunks_done = false;
     if constexpr (kPost && (MODE & MODE_ASSOC) != 0) {
-        if (!map_mode && a.off_recs >= 0) {
+        if (!map_mode && a.off_recs >= 0 && recs_fit) {
             post_assoc_fast(a, s, c0, nchunks, id0, lmk, vis, L, corg, smem + a.off_recs, lane);
             chunks_done = true;
         }
@@ -2832,6 +2841,7 @@ struct lslam_ctx {
     // waiting for that call's fix-up; the fix-up replays the scans it replayed (spec_dirty)
     int speculate;            // env LSLAM_MT_SPECULATE=0: wait for the fix-up (A/B)
     int spec_ok;              // the previous call was a one-epoch pipeline call with dirty flags
+    int spec_run;             // consecutive speculative calls (bounded by LSLAM_SPEC_RESYNC)
     const uint32_t *prev_state_scr;
     int prev_spec_scans;
     uint8_t *spec_dirty[2];   // [n_scans] replayed-by-fix-up flags, by call parity
@@ -2968,6 +2978,7 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->speculate = 1;
     if (const char *e = getenv("LSLAM_MT_SPECULATE")) c->speculate = atoi(e) != 0;
     c->spec_ok = 0;
+    c->spec_run = 0;
     c->prev_state_scr = nullptr;
     c->prev_spec_scans = 0;
     c->spec_dirty[0] = c->spec_dirty[1] = nullptr;
@@ -3787,6 +3798,14 @@ static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
     return x < y + nb && y < x + na;
 }
 
+// did a copy since the producer last synchronised with ev_copy write [p, p + n)?
+static bool copy_unknown_or_hits(const lslam_ctx *c, const void *p, size_t n) {
+    if (c->copy_unknown) return true;
+    for (int j = 0; j < c->n_copy_rng; j++)
+        if (ranges_overlap(p, n, c->copy_rng[j].p, c->copy_rng[j].n)) return true;
+    return false;
+}
+
 // did a copy since the producer last synchronised with ev_copy write one of its inputs?
 static bool copy_hazard(const lslam_ctx *c, const lslam_scan_batch *b) {
     if (c->copy_unknown) return true;
@@ -4062,6 +4081,9 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         // producer on its own stream: it waits for its slot's previous consumers, for input
         // copies, and (on a hazard) for the previous call; the consumers wait for it
         HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
+        // a copy into this call's MT state (e.g. a caller's upload into the previous call's
+        // mt_state_out) invalidates speculating from the previous producer's end state
+        const bool state_copied = copy_unknown_or_hits(c, b->mt_state_in, (size_t)b->n_scans * 625 * 4);
         if (copy_hazard(c, b)) {
             HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
             c->n_copy_rng = 0;
@@ -4079,7 +4101,13 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         // producer's end state, which precedes this producer on pstream, instead of waiting for
         // the previous fix-up; this call's fix-up replays the scans that one replayed
         spec = hz == 1 && c->speculate && c->spec_ok && k.ep_count == 1 && c->prev_state_scr &&
-               c->prev_spec_scans == b->n_scans && b->mt_state_in == c->prev_state_out;
+               c->prev_spec_scans == b->n_scans && b->mt_state_in == c->prev_state_out && !state_copied;
+        // a scan replayed by a speculative call stays dirty in every later one (its producer state
+        // is never repaired): every LSLAM_SPEC_RESYNC-th chained call (default 32)
+        // waits for the previous fix-up instead, which clears the flags
+        static const int spec_resync = [] { const char *e = getenv("LSLAM_SPEC_RESYNC"); const int v = e ? atoi(e) : 32; return v > 0 ? v : 32; }();
+        if (spec && ++c->spec_run >= spec_resync) spec = false;
+        if (!spec) c->spec_run = 0;
         if (hz == 1 && !spec) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
         // a producer that waited on the previous call will most likely wait on this one too, so
         // this call's resolve runs alone: the LDS-staged form is faster there (map mode 1.48 vs
@@ -4268,6 +4296,7 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     c->prev_slot = last;
     c->prev_fixed = b->mt_state_out ? 1 : 0;
     c->spec_ok = 0;
+    c->spec_run = 0;
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_HYP);
 }

@@ -74,3 +74,43 @@ def test_speculative_chain_equals_waiting_chain(stoppers):
     if stoppers:
         stop = (a[1]["models"]["flags"] & 16) != 0
         assert stop[np.array([sco[s] + 2 for s in stoppers])].all()  # the replay path ran
+
+
+def test_state_upload_between_chained_calls_disables_speculation():
+    """A caller writing the previous call's mt_state_out between two chained calls (here a
+    DeviceArray.upload of other streams' states) must be what the next call parses from: the
+    speculative context equals the waiting one and a fresh pipeline seeded from that state."""
+    from lidar_slam_amd.pipeline import ScanPipeline, mt_seed_state
+    spec, wait = _contexts()
+    xy, sco, cpo = _batch(128, (3, 40))
+    S = len(sco) - 1
+    new_state = np.stack([mt_seed_state(1000 + s) for s in range(S)])
+    outs = []
+    for ctx in (spec, wait):
+        p0 = ScanPipeline(ctx, xy, sco, cpo, seeds=np.arange(S, dtype=np.uint32), lmk_capacity=64, want_state=True)
+        p1 = ScanPipeline(ctx, xy, sco, cpo, mt_state=p0.state_out, lmk_capacity=64, want_draws=True,
+                          want_state=True)
+        p0.run(sync=False)
+        p0.state_out.upload(new_state)
+        p1.run(sync=False)
+        ctx.sync()
+        outs.append(p1.results())
+    fresh = ScanPipeline(spec, xy, sco, cpo, mt_state=new_state, lmk_capacity=64, want_draws=True, want_state=True)
+    fresh.run()
+    rf = fresh.results()
+    for r in outs:
+        assert np.array_equal(r["draws"], rf["draws"])
+        assert np.array_equal(r["mt_state"], rf["mt_state"])
+        assert np.array_equal(r["mask"], rf["mask"])
+
+
+def test_long_speculative_chain_resyncs():
+    """40 chained calls with early-stopping scans (past the LSLAM_SPEC_RESYNC bound of 32, where
+    one call waits for the previous fix-up and the replay flags clear) equal the waiting chain."""
+    spec, wait = _contexts()
+    xy, sco, cpo = _batch(64, (1, 9, 30))
+    a = _chain(spec, xy, sco, cpo, 40)
+    b = _chain(wait, xy, sco, cpo, 40)
+    for k, (ra, rb) in enumerate(zip(a, b)):
+        assert np.array_equal(ra["mt_state"], rb["mt_state"]), "call %d end states" % k
+        assert np.array_equal(ra["draws"], rb["draws"]), "call %d draws" % k

@@ -1,8 +1,10 @@
 """The C4 split / gather bookkeeping (lidar_slam_amd/shard.py) on CPU: a batch split
 across ranks, each rank's results gathered to the root in rank order, equals the
 single-process run bit for bit.  world_size 2 over gloo (127.0.0.1); the per-rank
-compute is the CPU oracle (this checks the partition and the gather, which the
-RCCL path shares: lidar_slam_amd/collective.py supplies the GPU transport)."""
+compute is the CPU oracle.  The gather runs collective.gatherv_plan's per-peer
+operations over gloo point-to-point, the same plan Comm.gatherv issues as grouped
+ncclSend / ncclRecv (the multi-rank RCCL execution itself needs >= 2 GPUs; RCCL
+refuses two ranks on one device, so it has not run on this builder's hardware)."""
 import os
 import socket
 
@@ -83,12 +85,24 @@ def _free_port():
 
 
 def _gloo_gatherv(dist, rank):
+    """collective.gatherv_plan executed over gloo point-to-point (the RCCL path runs the same
+    ops as grouped ncclSend / ncclRecv): checks the plan's peers, offsets, counts and
+    directions, not just shard.gather's bookkeeping."""
+    import torch
+
+    from lidar_slam_amd.collective import gatherv_plan
+
     def gatherv(send, recv, counts, root):
-        mine = np.ascontiguousarray(send).view(np.uint8).ravel()[:counts[rank]].tobytes()
-        objs = [None] * dist.get_world_size() if rank == root else None
-        dist.gather_object(mine, objs, dst=root)
-        if rank == root:
-            recv[:] = np.frombuffer(b"".join(objs), np.uint8)
+        src = np.ascontiguousarray(send).view(np.uint8).ravel()
+        for kind, peer, off, n in gatherv_plan(rank, dist.get_world_size(), counts, root):
+            if kind == "copy":
+                recv[off:off + n] = src[:n]
+            elif kind == "send":
+                dist.send(torch.from_numpy(src[off:off + n].copy()), dst=peer)
+            else:
+                buf = torch.empty(n, dtype=torch.uint8)
+                dist.recv(buf, src=peer)
+                recv[off:off + n] = buf.numpy()
     return gatherv
 
 
@@ -112,6 +126,14 @@ def _worker(rank, world, port, out):
                        lmk_capacity=cap)
     if rank == 0:
         out["got"] = {k: shard.host_view(k, v, len(ids), cap).tobytes() for k, v in got.items()}
+    # ragged transfers with a zero-count rank on either side, and a non-zero root
+    gv = _gloo_gatherv(dist, rank)
+    for counts, root in (([37, 0], 0), ([0, 29], 0), ([0, 29], 1), ([11, 5], 1), ([0, 0], 0)):
+        send = (np.arange(64) + 100 * rank).astype(np.uint8)
+        recv = np.full(sum(counts), 255, np.uint8) if rank == root else None
+        gv(send, recv, counts, root)
+        if rank == root:
+            out["gv%s_%d" % (counts, root)] = recv.tobytes()
     dist.destroy_process_group()
 
 
@@ -130,3 +152,26 @@ def test_two_rank_gloo_split_gather_equals_single_run():
     assert set(got) == set(shard.FIELDS)
     for k in shard.FIELDS:
         assert got[k] == np.ascontiguousarray(ref[k]).tobytes(), k
+    for counts, root in (([37, 0], 0), ([0, 29], 0), ([0, 29], 1), ([11, 5], 1), ([0, 0], 0)):
+        want = b"".join((np.arange(64) + 100 * r).astype(np.uint8)[:n].tobytes() for r, n in enumerate(counts))
+        assert out["gv%s_%d" % (counts, root)] == want, (counts, root)
+
+
+def test_gatherv_plan():
+    from lidar_slam_amd.collective import gatherv_plan
+    counts = [5, 0, 7, 3]
+    assert gatherv_plan(0, 4, counts) == [("copy", 0, 0, 5), ("recv", 2, 5, 7), ("recv", 3, 12, 3)]
+    assert gatherv_plan(1, 4, counts) == []                       # zero-count rank: nothing
+    assert gatherv_plan(2, 4, counts) == [("send", 0, 0, 7)]
+    assert gatherv_plan(2, 4, counts, root=2) == [("copy", 2, 5, 7), ("recv", 0, 0, 5), ("recv", 3, 12, 3)]
+    assert gatherv_plan(0, 1, [9]) == [("copy", 0, 0, 9)]
+    # the root's receives tile recv exactly: every rank's bytes at sum(counts[:r])
+    for root in range(4):
+        ops = gatherv_plan(root, 4, counts, root)
+        spans = sorted((off, off + n) for _, _, off, n in ops)
+        assert spans[0][0] == 0 and spans[-1][1] == sum(counts)
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    for bad in (dict(rank=0, world=2, counts=[1]), dict(rank=0, world=2, counts=[1, -1]),
+                dict(rank=2, world=2, counts=[1, 1]), dict(rank=0, world=2, counts=[1, 1], root=2)):
+        with pytest.raises(ValueError):
+            gatherv_plan(**bad)
