@@ -121,10 +121,12 @@ def _solve7(M, v):
 
 
 def step(x, P, u, z, lmk, R_diag, dt=DT, Q=None, alpha=1e-4, beta=2.0, kappa=0.0, predict=True, update=True,
-         dense=False):
+         dense=False, sigmas=None):
     """One predict + update (either may be skipped) of one filter.  Arguments are float64
     arrays; returns (x[3], P[3][3]) as mpf lists.  ``dense`` applies S^-1 by an LU solve of
-    the 2L x 2L S instead of the Woodbury form (the cross-check)."""
+    the 2L x 2L S instead of the Woodbury form (the cross-check).  ``sigmas`` (7 x 3 float64,
+    update only): filterpy's cached sigmas_f, used with the given x and P instead of sigma
+    points drawn from them (filterpy's update after x or P was reassigned)."""
     with mp.workdps(DPS):
         Wm, Wc, lpn = weights(alpha, beta, kappa)
         xs = [_f(v) for v in np.asarray(x, np.float64).reshape(3)]
@@ -145,7 +147,10 @@ def step(x, P, u, z, lmk, R_diag, dt=DT, Q=None, alpha=1e-4, beta=2.0, kappa=0.0
             Ps = [[Pn[i][j] + Qs[i][j] for j in range(3)] for i in range(3)]
         if not update:
             return xs, Ps
-        sf = sigma_points(xs, Ps, lpn)
+        if sigmas is not None and not predict:
+            sf = [[_f(v) for v in row] for row in np.asarray(sigmas, np.float64).reshape(7, 3)]
+        else:
+            sf = sigma_points(xs, Ps, lpn)
         lm = [(_f(px), _f(py)) for px, py in np.asarray(lmk, np.float64).reshape(-1, 2)]
         sh = [hx(s, lm) for s in sf]
         zp = z_mean(sh, Wm)

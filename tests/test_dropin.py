@@ -217,13 +217,21 @@ def test_ukf_dropin_arguments_are_strict():
 def test_system_ukf_keeps_filterpy_state():
     """filterpy keeps sigmas_f from predict: update uses them with the CURRENT x and P, so
     predict -> set x -> update, update twice, and update before any predict (sigmas_f = 0)
-    follow oracle/ukf.py's UKF (the same state handling) to 1e-5 per component."""
+    follow filterpy's state handling.  The drop-in and oracle/ukf.py's UKF (the same state
+    handling in NumPy) are both held to the 50-digit evaluation of that step on the same
+    cached sigma points (oracle/ukf_exact.step(sigmas=...)): x, y, theta at 1e-5.  P at 1e-3
+    relative: with x moved by d off the sigma points' mean, P - K S K^T cancels terms scaled
+    by the ~1e8 weights, and float64 P errors grow as ~1e-3 |d| (measured on the oracle: 3e-4
+    at this d, 3e-3 at ten times it).  The two semantics differ far beyond those bounds (the
+    re-drawn sigma points move theta by ~8e-3 here), so the test tells them apart."""
     from oracle import ukf as oukf
-    from oracle import ukf_exact
+    from oracle import ukf_exact as ux
     rng = np.random.default_rng(7)
     lm = [tuple(p) for p in rng.uniform(-3000, 3000, (8, 2))]
     x0 = np.array([1000.0, 800.0, 0.3])
     z = oukf.transfer_function(x0, lm) + rng.normal(0, 0.2, 16)
+    Rd = np.array([0.25, 0.09] * 8)
+    d = np.array([0.3, -0.2, 0.001])
 
     def both():
         sysm = systemClass.System([])
@@ -231,24 +239,29 @@ def test_system_ukf_keeps_filterpy_state():
         sysm.ukf.x, f.x = x0.copy(), x0.copy()
         return sysm.ukf, f
 
-    def close(g, f):
-        err = ukf_exact.component_errors(g.x[None], g.P[None], f.x[None], f.P[None])
-        assert max(err.values()) <= 1e-5, err
+    def update_both(g, f):
+        xe, Pe = ux.to_float(*ux.step(g.x, g.P, (0, 0), z, np.array(lm), Rd, predict=False, sigmas=g.sigmas_f))
+        xr, Pr = ux.to_float(*ux.step(g.x, g.P, (0, 0), z, np.array(lm), Rd, predict=False))  # re-drawn
+        assert ux.component_errors(xr[None], Pr[None], xe[None], Pe[None])["theta_abs"] > 1e-3
+        g.update(z, landmarks=lm)
+        f.update(z, lm)
+        for h in (g, f):
+            err = ux.component_errors(h.x[None], h.P[None], xe[None], Pe[None])
+            assert max(err["x_rel"], err["y_rel"], err["theta_abs"]) <= 1e-5, (type(h).__module__, err)
+            assert err["P_rel"] <= 1e-3, (type(h).__module__, err)
 
     g, f = both()                                   # predict -> set x -> update
     g.predict(u=[2.0, 2.5])
     f.predict(np.array([2.0, 2.5]))
     assert np.allclose(g.sigmas_f, f.sigmas_f, rtol=1e-9, atol=1e-9)
-    g.x = f.x = f.x + np.array([3.0, -2.0, 0.01])
-    g.update(z, landmarks=lm)
-    f.update(z, lm)
-    close(g, f)
-    g.update(z, landmarks=lm)                       # a second update reuses the same sigmas_f
-    f.update(z, lm)
-    close(g, f)
+    f.sigmas_f = g.sigmas_f.copy()                  # the same cached points on both sides
+    g.x = f.x = f.x + d
+    g.P = f.P = g.P.copy()
+    update_both(g, f)
+    update_both(g, f)                               # a second update reuses the same sigmas_f
     g, f = both()                                   # update first: filterpy's zero sigmas_f
     assert not np.any(g.sigmas_f)
     g.P = f.P = np.diag([4.0, 4.0, 0.01])
     g.update(z, landmarks=lm)
     f.update(z, lm)
-    assert np.all(np.isfinite(g.x)) and np.allclose(g.x, f.x, rtol=1e-6, atol=1e-6)
+    assert np.array_equal(g.x, x0) and np.array_equal(f.x, x0)   # K = 0: every sigma maps to one point

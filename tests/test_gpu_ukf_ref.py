@@ -6,7 +6,10 @@ lane-group UKF step of lslam_ukf_step with extra stores.
 
 Bounds, all stated here:
 * hx(sigma_0) against the fixture (update-only step: sigma_0 = x exactly): distances
-  BIT-EXACT (fl(fl(dx^2) + fl(dy^2)) and a correctly rounded sqrt on both sides);
+  within 1 ulp, and bit-exact for at least 99 % of them: the kernel squares with one
+  correctly rounded multiply, the reference with ``(px - x[0])**2`` (UKFMethods.py:31),
+  i.e. glibc's pow(d, 2), which is 1 ulp off d*d for a few arguments (3 of the 800 c5
+  distances); the sum and the square root round identically;
   bearings within BEARING_ULP ulp of max(pi, |theta|), compared modulo 2 pi (the GPU's
   atan2 is OCML's, the reference's glibc's; both are faithful, not correctly rounded).
   The edge case's landmarks dead ahead / dead behind (atan2 = +0 / pi exactly on both
@@ -56,8 +59,11 @@ def _bearing_err(a, b):
 
 
 def _check_hx(hx_gpu, hx_ref, theta):
-    """distances bit-exact, bearings within BEARING_ULP ulp of max(pi, |theta|) modulo 2 pi"""
-    assert np.array_equal(_bits(hx_gpu[..., 0::2]), _bits(hx_ref[..., 0::2]))
+    """distances within 1 ulp (>= 99 % bit-exact), bearings within BEARING_ULP ulp of
+    max(pi, |theta|) modulo 2 pi"""
+    dg, dr = hx_gpu[..., 0::2], hx_ref[..., 0::2]
+    assert np.all(np.abs(dg - dr) <= np.spacing(dr))
+    assert np.mean(dg == dr) >= 0.99
     tol = BEARING_ULP * np.spacing(np.maximum(np.pi, np.abs(theta)))
     err = _bearing_err(hx_gpu[..., 1::2], hx_ref[..., 1::2])
     assert np.all(err <= tol[..., None]), float(np.max(err / tol[..., None]))
