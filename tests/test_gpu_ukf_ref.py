@@ -59,14 +59,14 @@ def _bearing_err(a, b):
 
 
 def _check_hx(hx_gpu, hx_ref, theta):
-    """distances within 1 ulp (>= 99 % bit-exact), bearings within BEARING_ULP ulp of
-    max(pi, |theta|) modulo 2 pi"""
+    """distances within 1 ulp, bearings within BEARING_ULP ulp of max(pi, |theta|) modulo
+    2 pi; returns (bit-exact distances, distances) for the caller's >= 99 % check"""
     dg, dr = hx_gpu[..., 0::2], hx_ref[..., 0::2]
     assert np.all(np.abs(dg - dr) <= np.spacing(dr))
-    assert np.mean(dg == dr) >= 0.99
     tol = BEARING_ULP * np.spacing(np.maximum(np.pi, np.abs(theta)))
     err = _bearing_err(hx_gpu[..., 1::2], hx_ref[..., 1::2])
     assert np.all(err <= tol[..., None]), float(np.max(err / tol[..., None]))
+    return int(np.sum(dg == dr)), dg.size
 
 
 @pytest.mark.parametrize("case", ["c3", "c5", "edge"])
@@ -75,7 +75,8 @@ def test_hx_sigma0_vs_reference(ctx, golden, case):
     t = _trace(ctx, g, case)
     x = g[case + "_x"]
     assert np.array_equal(_bits(t["sigmas"][:, 0]), _bits(x))  # update-only: sigma_0 = x
-    _check_hx(t["hx"][:, 0], g[case + "_hx"], x[:, 2])
+    same, n = _check_hx(t["hx"][:, 0], g[case + "_hx"], x[:, 2])
+    assert same >= 0.99 * n, (same, n)
     if case == "edge":
         # dead ahead: bearing = normalize_angle(a); dead behind: normalize_angle(pi + a) -- bit-exact
         assert np.array_equal(_bits(t["hx"][:, 0, 1]), _bits(g["edge_hx"][:, 1]))
@@ -100,6 +101,9 @@ def test_hx_all_sigmas_vs_oracle(ctx, golden, case):
     g = golden("ukf_ref.npz")
     t = _trace(ctx, g, case)
     lm = g[case + "_lmk"]
+    same = n = 0
     for s in range(len(lm)):
         want = np.stack([oukf.transfer_function(t["sigmas"][s, k], [tuple(p) for p in lm[s]]) for k in range(7)])
-        _check_hx(t["hx"][s], want, t["sigmas"][s, :, 2])
+        a, b = _check_hx(t["hx"][s], want, t["sigmas"][s, :, 2])
+        same, n = same + a, n + b
+    assert same >= 0.99 * n, (same, n)
