@@ -571,7 +571,12 @@ def main():
         roof = {"bound": "fp64-valu", "achieved": round(cons_tf, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "traffic": traffic_of("chunk_kernel"),
                 "kernel": "chunk_kernel (consensus A4-A8)", "kernel_ms": round(cavg, 4), "flops_per_launch": flops}
+    step_tf = flops / (elapsed / args.steps) / 1e12
     roof.update({
+        # SURVEY §8(d)'s definition over the whole step: algorithmic FP64 flops per step (12 per
+        # point-hypothesis evaluation) / the timed ms_per_step / the FP64 vector peak
+        "step_fp64_tflops": round(step_tf, 4),
+        "step_fp64_frac": round(step_tf / FP64_PEAK_TFLOPS, 5),
         "consensus": {"kernel": "chunk_kernel", "ms": round(cavg, 4), "fp64_tflops": round(cons_tf, 4),
                       "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "flops_per_launch": flops},
         "pipeline": {"ms": round(kavg, 4), "alg_bytes_per_launch": alg_bytes, "hbm_alg_gbs": round(hbm_gbs, 2),

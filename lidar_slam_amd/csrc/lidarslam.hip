@@ -1644,6 +1644,9 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
     if (wave < PPW) {
         const int s = (int)blockIdx.x * PPW + wave;
         RngPipe rp = pipe_of(wave);
+#ifdef LSLAM_WSTAMPS
+        for (int k = 0; k < 8; k++) rp.wacc[k] = 0;
+#endif
 #ifdef LSLAM_STAMPS
         for (int k = 0; k < 8; k++) rp.acc[k] = 0;
         const uint64_t t_start = lslam_stamp();
@@ -1701,7 +1704,15 @@ __global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
         rp.acc[7] = lslam_stamp() - t_start;
         rp.acc[4] = rt_start;  // residency census (100 MHz chip-wide clock)
         rp.acc[3] = __builtin_amdgcn_s_memrealtime();
+#ifdef LSLAM_WSTAMPS
         if (a.dbg && lane == 0) {
+            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
+            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + 8 + k] = rp.wacc[k];
+        }
+        if (false) {
+#else
+        if (a.dbg && lane == 0) {
+#endif
             for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
             // placement census: HW_ID simd / cu / se of the parser, xcc
             a.dbg[(size_t)s * 16 + 8] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));

@@ -136,6 +136,9 @@ struct RngPipe {
 #ifdef LSLAM_STAMPS
     uint64_t acc[8];
 #endif
+#ifdef LSLAM_WSTAMPS
+    uint64_t wacc[8];
+#endif
 };
 
 // Level RP_PRIO_TOP - floor(3 done / (total + 1)): two compares against thresholds set
@@ -167,8 +170,14 @@ __device__ __forceinline__ void rp_need_block(RngPipe &rp, int need, int lane) {
 }
 
 // Diagnostic build only: parser cycle accounting (0 block waits, 2 fixed point,
-// 3 rest of the window, 5 windows, 6 fixed-point evaluations)
-#ifdef LSLAM_STAMPS
+// 3 rest of the window, 5 windows, 6 fixed-point evaluations).  With LSLAM_WSTAMPS
+// as well, those are off and the table-mode windows inside a run (tbl_window<false>)
+// are cut into segments instead (rp.wacc, tools/wstamps.py): 0 next window's word
+// load + temper, 1 reject-table read + funnel shifts, 2 the unchecked evaluations,
+// 3 the checked loop (convergence tests, branches, further evaluations), 4 store and
+// window bookkeeping; 5 windows, 6 checked iterations, 7 an empty segment (the
+// stamp's own cost, to subtract from each segment).
+#if defined(LSLAM_STAMPS) && !defined(LSLAM_WSTAMPS)
 #define RP_STAMP_DECL uint64_t _rp_prev = lslam_stamp();
 #define RP_STAMP(k)                         \
     do {                                    \
@@ -380,6 +389,11 @@ __device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
     return (y ^ (y >> 18)) & mK;
 }
 
+// evaluations after the first one before the first convergence check (tbl_window)
+#ifndef LSLAM_TBL_UNCHECKED
+#define LSLAM_TBL_UNCHECKED 3
+#endif
+
 typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
 __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
     // 32-bit LDS byte address: v * 28 (v <= 127) as one u24 multiply-add onto the scalar
@@ -417,32 +431,68 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
         asm volatile("" ::: "memory");
         raw = kb[pos + lane];
     }
+#ifdef LSLAM_WSTAMPS
+    const bool wst = !CHECK;
+    uint64_t _w = wst ? lslam_stamp() : 0;
+#define WSTAMP(k)                                  \
+    do {                                           \
+        if (wst) {                                 \
+            const uint64_t _t = lslam_stamp();     \
+            rp.wacc[k] += _t - _w;                 \
+            _w = _t;                               \
+        }                                          \
+    } while (0)
+    if (wst) {
+        WSTAMP(7);
+        rp.wacc[5] += 1;
+    }
+#else
+#define WSTAMP(k) do {} while (0)
+#endif
     // next window's words (after a crossing window: discarded by the block switch)
     const uint32_t nraw = kb[pos + 64 + lane];
     const uint32_t v = rt_temper_mask(raw, mK);
+    WSTAMP(0);
     const uint64_t M = rt_window(rp.tbl, v, sg);
+#ifdef LSLAM_WSTAMPS
+    if (wst) asm volatile("" ::"v"((uint32_t)M), "v"((uint32_t)(M >> 32)));
+#endif
+    WSTAMP(1);
     // three evaluations without a convergence check (one more evaluation of the fixed point
     // leaves it unchanged; ~5 are needed on average), then one per check: fewer VALU -> SALU
     // round trips and branches
     uint64_t R = ballot(rt_rej(M, s0));
 #pragma unroll
-    for (int e = 0; e < 3; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
+    for (int e = 0; e < LSLAM_TBL_UNCHECKED; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
+#ifdef LSLAM_WSTAMPS
+    if (wst) asm volatile("" ::"s"(R));
+#endif
+    WSTAMP(2);
     uint32_t s;
     RP_COUNT(6, 4);
     for (;;) {
         s = mbcnt_from(R, sbase);
         const uint64_t Rn = ballot(rt_rej(M, s));
         RP_COUNT(6, 1);
+#ifdef LSLAM_WSTAMPS
+        if (wst) rp.wacc[6] += 1;
+#endif
         if (Rn == R) break;
         R = Rn;
     }
     RP_COUNT(5, 1);
+    WSTAMP(3);
     store_accepted(J, gq - s, v, R);
     const uint32_t na = accepted_count(R);
     pos += 64;
     gq += na;
     sg = rt_wrap<KGE64>(sg + na, K);
     raw = nraw;
+#ifdef LSLAM_WSTAMPS
+    if (wst) asm volatile("" ::"s"(sg), "s"(gq));
+#endif
+    WSTAMP(4);
+#undef WSTAMP
 }
 
 template <bool KGE64, typename JT>
