@@ -391,7 +391,7 @@ __device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
 
 // evaluations after the first one before the first convergence check (tbl_window)
 #ifndef LSLAM_TBL_UNCHECKED
-#define LSLAM_TBL_UNCHECKED 3
+#define LSLAM_TBL_UNCHECKED 2
 #endif
 
 typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
@@ -458,9 +458,12 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     if (wst) asm volatile("" ::"v"((uint32_t)M), "v"((uint32_t)(M >> 32)));
 #endif
     WSTAMP(1);
-    // three evaluations without a convergence check (one more evaluation of the fixed point
-    // leaves it unchanged; ~5 are needed on average), then one per check: fewer VALU -> SALU
-    // round trips and branches
+    // LSLAM_TBL_UNCHECKED evaluations after the first without a convergence check (one more
+    // evaluation of the fixed point leaves it unchanged; ~4.5 reach it on average), then one per
+    // check.  Two (three evaluations before the first check) measured fastest at r04 (C3 step
+    // 0.777 vs 0.793 ms with three): the producer's VALU count, not its checks' latency, is what
+    // the consumers beside it feel.  A count-based test (converged when mbcnt(R) repeats the
+    // counts, which needs no confirming evaluation) was slower: 6 VALU per checked turn.
     uint64_t R = ballot(rt_rej(M, s0));
 #pragma unroll
     for (int e = 0; e < LSLAM_TBL_UNCHECKED; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
@@ -469,7 +472,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
 #endif
     WSTAMP(2);
     uint32_t s;
-    RP_COUNT(6, 4);
+    RP_COUNT(6, 1 + LSLAM_TBL_UNCHECKED);
     for (;;) {
         s = mbcnt_from(R, sbase);
         const uint64_t Rn = ballot(rt_rej(M, s));
