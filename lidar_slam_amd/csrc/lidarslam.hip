@@ -397,18 +397,47 @@ __device__ __forceinline__ double sd(unsigned lo, unsigned hi) {
 
 // one point against the lane's hypothesis: r = fl(x uy - fl(y ux + k)),
 // S += r^2, lo += |r| <= r_lo, hi += |r| < r_hi
+#ifndef LSLAM_COUNT_F64CMP
+// The two cutoffs are tested on r's HIGH dword read as a float (sign, exponent and the top 20
+// mantissa bits of the double; for non-negative values its order is the double's): the sure
+// inliers are |hi(r)| < hi(r_lo) (so |r| < r_lo), the possible ones |hi(r)| <= hi(r_hi) (every
+// |r| < r_hi).  A point between them (|r| within 2^-20 relative of the threshold, ~15 nm at
+// 20 mm) makes lo != hi, and the lane recounts exactly, as for the band.  Two FP32 compares
+// with the free |.| modifier instead of two FP64 compares (half rate on CDNA4).
+typedef float cut_t;
+__device__ __forceinline__ cut_t count_cut(double c) { return __uint_as_float((uint32_t)(__double_as_longlong(c) >> 32)); }
+__device__ __forceinline__ bool sure_in(double r, cut_t c) { return __builtin_fabsf(count_cut(r)) < c; }
+__device__ __forceinline__ bool maybe_in(double r, cut_t c) { return __builtin_fabsf(count_cut(r)) <= c; }
+__device__ __forceinline__ void count_one(double x, double y, double ux, double uy, double k, cut_t c_lo,
+                                          cut_t c_hi, int &lo, int &hi, double &S) {
+    // r = fma(x, uy, -fma(y, ux, k)) as two three-address FMAs (left to itself the compiler
+    // turns some into v_fmac + a 64-bit copy of k)
+    double t, r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(t) : "s"(y), "v"(ux), "v"(k));
+    asm("v_fma_f64 %0, %1, %2, -%3" : "=v"(r) : "s"(x), "v"(uy), "v"(t));
+    S = __builtin_fma(r, r, S);
+    lo += sure_in(r, c_lo) ? 1 : 0;
+    hi += maybe_in(r, c_hi) ? 1 : 0;
+    asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
+}
+#else
+typedef double cut_t;
+__device__ __forceinline__ cut_t count_cut(double c) { return c; }
+__device__ __forceinline__ bool sure_in(double r, cut_t c) { return fabs(r) <= c; }
+__device__ __forceinline__ bool maybe_in(double r, cut_t c) { return fabs(r) < c; }
 __device__ __forceinline__ void count_one(double x, double y, double ux, double uy, double k, double r_lo,
                                           double r_hi, int &lo, int &hi, double &S) {
     const double r = __builtin_fma(x, uy, -__builtin_fma(y, ux, k));
     S = __builtin_fma(r, r, S);
-    lo += (fabs(r) <= r_lo) ? 1 : 0;
-    hi += (fabs(r) < r_hi) ? 1 : 0;
+    lo += sure_in(r, r_lo) ? 1 : 0;
+    hi += maybe_in(r, r_hi) ? 1 : 0;
     asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
 }
+#endif
 
 // one hypothesis per lane against all N points (gP: global, wave-uniform)
 __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, double ux, double uy, double k,
-                                                  double r_lo, double r_hi, int &lo, int &hi, double &S) {
+                                                  cut_t r_lo, cut_t r_hi, int &lo, int &hi, double &S) {
     int p = 0;
     if (N >= 4) {
         // two SGPR buffers in turn, so no copies between the load and its use
@@ -442,8 +471,8 @@ __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, doub
 }
 
 // the same from the LDS copy (polar batches: points converted on load)
-__device__ __forceinline__ void count_points_lds(const double2 *P, int N, double ux, double uy, double k, double r_lo,
-                                                 double r_hi, int &lo, int &hi, double &S) {
+__device__ __forceinline__ void count_points_lds(const double2 *P, int N, double ux, double uy, double k, cut_t r_lo,
+                                                 cut_t r_hi, int &lo, int &hi, double &S) {
     int p = 0;
     for (; p + 2 <= N; p += 2) {
         const double2 q0 = P[p], q1 = P[p + 1];
@@ -516,6 +545,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
     const double Rb = unid(fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx)));
     const double margin = (E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
     const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
+    const cut_t c_lo = count_cut(r_lo), c_hi = count_cut(r_hi);
     int M = 0;
     CH_STAMP(1);
     for (int tb = 0; tb < T; tb += 64) {
@@ -527,8 +557,8 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
         const double k = __builtin_fma(m.ox, m.uy, -(m.oy * m.ux));
         int lo = 0, hi = 0;
         double S = 0.0;
-        if (gP) count_points_sgpr(gP, N, m.ux, m.uy, k, r_lo, r_hi, lo, hi, S);
-        else count_points_lds(P, N, m.ux, m.uy, k, r_lo, r_hi, lo, hi, S);
+        if (gP) count_points_sgpr(gP, N, m.ux, m.uy, k, c_lo, c_hi, lo, hi, S);
+        else count_points_lds(P, N, m.ux, m.uy, k, c_lo, c_hi, lo, hi, S);
         int c = lo;
         if (exact_all || lo != hi) {  // rare: lane-divergent exact recount
             c = 0;
@@ -2488,6 +2518,7 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     const double margin = (bx.E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
     // c2 < ecut - margin  <=>  |r| <= r_lo;   c2 > ecut + margin  <=>  |r| >= r_hi
     const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
+    const cut_t c_lo = count_cut(r_lo), c_hi = count_cut(r_hi);
     cdouble_t *mp = (cdouble_t *)(a.models + ((size_t)c * T + t0) * 4);
     const double nan = __builtin_nan("");
     if (cheap) {
@@ -2512,8 +2543,8 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
 #pragma unroll
                 for (int j = 0; j < PPL; j++) {
                     const double r = __builtin_fma(qx[j], uy, -__builtin_fma(qy[j], ux, k));
-                    nlo += (uint32_t)popc64(ballot(fabs(r) <= r_lo));
-                    nhi += (uint32_t)popc64(ballot(fabs(r) < r_hi));
+                    nlo += (uint32_t)popc64(ballot(sure_in(r, c_lo)));
+                    nhi += (uint32_t)popc64(ballot(maybe_in(r, c_hi)));
                 }
                 const bool mine = lane == (t & 63);
                 acc_lo = mine ? (int)nlo : acc_lo;

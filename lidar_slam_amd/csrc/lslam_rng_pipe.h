@@ -473,6 +473,32 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     WSTAMP(2);
     uint32_t s;
     RP_COUNT(6, 1 + LSLAM_TBL_UNCHECKED);
+#ifdef LSLAM_TBL_LATECHECK
+    // The test of R_{k+1} == R_k reads the ballot one evaluation late: R_{k+2} is issued first,
+    // so the scalar compare finds R_{k+1}'s VALU result long done instead of waiting on it (the
+    // wait is most of a turn: ~140 of a window's ~760 cycles per checked turn, producer alone).
+    // One evaluation more per window (R_{k+2} = R_k once converged, discarded).  Three turns
+    // in a row rotate three ballots (ra, rb, rc) and their counts, so no turn copies a ballot
+    // that its own evaluation has just written.
+    uint64_t ra = R, rb, rc;
+    uint32_t sa = mbcnt_from(ra, sbase), sb, sc;
+    rb = ballot(rt_rej(M, sa));
+#define TBL_LATE_TURN(X, SX, Y, SY, Z, SZ)          \
+    SY = mbcnt_from(Y, sbase);                      \
+    Z = ballot(rt_rej(M, SY));                      \
+    __builtin_amdgcn_sched_barrier(0);              \
+    if (Y == X) {                                   \
+        R = X;                                      \
+        s = SX;                                     \
+        break;                                      \
+    }
+    for (;;) {
+        TBL_LATE_TURN(ra, sa, rb, sb, rc, sc)
+        TBL_LATE_TURN(rb, sb, rc, sc, ra, sa)
+        TBL_LATE_TURN(rc, sc, ra, sa, rb, sb)
+    }
+#undef TBL_LATE_TURN
+#else
     for (;;) {
         s = mbcnt_from(R, sbase);
         const uint64_t Rn = ballot(rt_rej(M, s));
@@ -483,6 +509,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
         if (Rn == R) break;
         R = Rn;
     }
+#endif
     RP_COUNT(5, 1);
     WSTAMP(3);
     store_accepted(J, gq - s, v, R);
