@@ -102,12 +102,27 @@ __device__ __forceinline__ int owning_scan(const lslam_scan_batch &B, int c) {
 
 enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8, MODE_POST = 16 };
 
+// A chunk's bounding-box terms and residual cutoffs (chunk_consensus, cut_finish).
+#ifndef LSLAM_COUNT_F64CMP
+typedef float cut_t;  // the count loops' cutoffs: FP32 on the residual's high dword (count_one)
+#else
+typedef double cut_t;
+#endif
+struct ChunkCut {
+    double tq;      // tie brackets: an upper bound of E2 + R (sqrt(E2) + 1) (tie_bound_q)
+    double margin;  // the exact-test band around ecut
+    cut_t c_lo, c_hi;
+    int finite;     // every point finite and the box bounds finite
+    int pad;
+};
+
 // ------------------------------------------------------------------------
 // kernel arguments (passed by value)
 // ------------------------------------------------------------------------
 struct KArgs {
     lslam_scan_batch b;
     double ecut;
+    double ecut_q;  // sqrt(ecut) * 1.01 + 1 (host)
     double thr;
     double tol_a, tol_b, tol_dist;
     uint64_t philox_seed;
@@ -365,6 +380,10 @@ __device__ __forceinline__ double tie_bound(double S, int N, double E2) {
 __device__ __forceinline__ double tie_bound_r(double S, int N, double E2, double R) {
     return ((double)N * (E2 + R * (sqrt(E2) + 1.0)) + (double)(N + 32) * S) * 0x1p-42;
 }
+// the same with tq >= E2 + R (sqrt(E2) + 1) made once per chunk (ChunkCut)
+__device__ __forceinline__ double tie_bound_q(double S, int N, double tq) {
+    return ((double)N * tq + (double)(N + 32) * S) * 0x1p-42;
+}
 
 // The count pass reads the chunk's points with scalar loads (through the
 // scalar cache, into SGPRs) when the batch holds Cartesian xy: every lane (a
@@ -404,7 +423,6 @@ __device__ __forceinline__ double sd(unsigned lo, unsigned hi) {
 // |r| < r_hi).  A point between them (|r| within 2^-20 relative of the threshold, ~15 nm at
 // 20 mm) makes lo != hi, and the lane recounts exactly, as for the band.  Two FP32 compares
 // with the free |.| modifier instead of two FP64 compares (half rate on CDNA4).
-typedef float cut_t;
 __device__ __forceinline__ cut_t count_cut(double c) { return __uint_as_float((uint32_t)(__double_as_longlong(c) >> 32)); }
 __device__ __forceinline__ bool sure_in(double r, cut_t c) { return __builtin_fabsf(count_cut(r)) < c; }
 __device__ __forceinline__ bool maybe_in(double r, cut_t c) { return __builtin_fabsf(count_cut(r)) <= c; }
@@ -421,7 +439,6 @@ __device__ __forceinline__ void count_one(double x, double y, double ux, double 
     asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
 }
 #else
-typedef double cut_t;
 __device__ __forceinline__ cut_t count_cut(double c) { return c; }
 __device__ __forceinline__ bool sure_in(double r, cut_t c) { return fabs(r) <= c; }
 __device__ __forceinline__ bool maybe_in(double r, cut_t c) { return fabs(r) < c; }
@@ -498,6 +515,107 @@ __device__ __forceinline__ void count_points_lds(const double2 *P, int N, double
 #define CH_STAMP_DECL
 #endif
 
+// The chunk's box as upper bounds, not the box itself: the high dword of each coordinate as a
+// signed-order key (key(-x) = ~key(x)), so max x, -min x, max y, -min y are four integer maxima
+// (per lane, then over the wave by DPP), and a key decodes to the largest double with that high
+// dword.  A looser E2 or R only widens the cutoffs' band and the tie brackets, both decided
+// exactly beyond them: the counts, winners and sums are the same bits.
+__device__ __forceinline__ int hkey(double d) {
+    const int h = (int)(__double_as_longlong(d) >> 32);
+    return h ^ ((h >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ double key_up(int k) {  // >= every double whose key is k
+    const int h = k ^ ((k >> 31) & 0x7fffffff);
+    return __longlong_as_double((long long)(((unsigned long long)(uint32_t)h << 32) | (h >= 0 ? 0xffffffffull : 0ull)));
+}
+__device__ __forceinline__ bool key_finite(int k) {
+    const int h = k ^ ((k >> 31) & 0x7fffffff);
+    return (h & 0x7ff00000) != 0x7ff00000;
+}
+struct BoxAcc {
+    int xh = INT_MIN, xl = INT_MAX, yh = INT_MIN, yl = INT_MAX;  // max / min key of x and y
+    __device__ __forceinline__ void add(double2 q) {
+        const int kx = hkey(q.x), ky = hkey(q.y);
+        xh = max(xh, kx);
+        xl = min(xl, kx);
+        yh = max(yh, ky);
+        yl = min(yl, ky);
+    }
+};
+__device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecut_q);
+template <typename PP>
+__device__ __forceinline__ ChunkCut chunk_cut(PP P, int N, double ecut, double ecut_q, int lane) {
+    BoxAcc b;
+    for (int p = lane; p < N; p += 64) b.add(P[p]);
+    return cut_finish(b, ecut, ecut_q);
+}
+
+// max over the wave (every lane active), uniform: DPP within rows of 16, the row broadcasts to
+// lane 63, one readlane -- no LDS round trips (beside the producer, whose parsers keep the LDS
+// busy, six ds_bpermute levels per value were most of the box's cost)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_max_step(int v) {
+    return max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, CTRL, ROWS, 0xf, false));  // INT_MIN where no source
+}
+__device__ __forceinline__ int wave_max_dpp(int v) {
+    v = dpp_max_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_max_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_max_step<0x124, 0xf>(v);  // row_ror:4
+    v = dpp_max_step<0x128, 0xf>(v);  // row_ror:8
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// High-dword cutoffs (count_one) without the exact square-root search: c_lo <= hi(sq_floor_lt(e)),
+// c_hi >= hi(sq_ceil_gt(e)).  v_sqrt_f32 of (float)e is within 2^-22 relative of the root, a
+// quarter of a high-dword unit; two units of slack leave the band only wider.  Outside float's
+// comfortable range, the exact search.
+__device__ __forceinline__ float hi_units(double s, int d) {
+    return __uint_as_float((uint32_t)(__double_as_longlong(s) >> 32) + (uint32_t)d);
+}
+__device__ __forceinline__ cut_t cut_lo_of(double e) {
+#ifndef LSLAM_COUNT_F64CMP
+    if (!(e > 0.0)) return -1.0f;
+    if (e >= 0x1p-100 && e <= 0x1p100) return hi_units((double)__builtin_amdgcn_sqrtf((float)e), -2);
+#endif
+    return count_cut(sq_floor_lt(e));
+}
+__device__ __forceinline__ cut_t cut_hi_of(double e) {
+#ifndef LSLAM_COUNT_F64CMP
+    if (e >= 0x1p-100 && e <= 0x1p100) return hi_units((double)__builtin_amdgcn_sqrtf((float)e), 2);
+#endif
+    return count_cut(sq_ceil_gt(e));
+}
+
+__device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecut_q) {
+    const int kxh = wave_max_dpp(b.xh), kxl = wave_max_dpp(~b.xl);  // keys of max x, -min x
+    const int kyh = wave_max_dpp(b.yh), kyl = wave_max_dpp(~b.yl);
+    ChunkCut cc;
+    cc.finite = key_finite(kxh) && key_finite(kxl) && key_finite(kyh) && key_finite(kyl);
+    const double hx = key_up(kxh), lx = key_up(kxl), hy = key_up(kyh), ly = key_up(kyl);
+    const double bx = hx + lx, by = hy + ly;  // >= max x - min x, max y - min y
+    const double E2 = (bx * bx + by * by) * (1.0 + 0x1p-20);
+    const double Rb = (fmax(hx, lx) + fmax(hy, ly)) * (1.0 + 0x1p-40);  // >= max|x| + max|y|
+    cc.finite = cc.finite && E2 < __builtin_inf();
+    cc.pad = 0;
+    cc.tq = 0.0;
+    cc.margin = 0.0;
+    cc.c_lo = count_cut(-1.0);
+    cc.c_hi = count_cut(0.0);
+    if (cc.finite && ecut < __builtin_inf()) {
+        // Reassociated cross product r = fl(x uy - fl(y ux + k)) (two fmas), k = ox uy - oy ux per
+        // hypothesis, with the band widened by the R sqrt(ecut) term (see count_kernel;
+        // ecut_q = sqrt(ecut) * 1.01 + 1 from the host) and tested as two cutoffs on |r|
+        cc.margin = (E2 + ecut + Rb * ecut_q) * 0x1p-42;
+        cc.c_lo = cut_lo_of(ecut - cc.margin);
+        cc.c_hi = cut_hi_of(ecut + cc.margin);
+        const double sE = (double)__builtin_amdgcn_sqrtf((float)E2) * (1.0 + 0x1p-20);  // >= sqrt(E2)
+        cc.tq = E2 + Rb * (sE + 1.0);
+    }
+    return cc;
+}
+
 __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const double2 *gP, int N, const int32_t *draws,
                                     int32_t *cnt, int32_t *tied, double *tsum, int32_t *inl, double *vtmp,
                                     double *vstack, int *nstack, int32_t *cnt_out, int lane,
@@ -505,29 +623,8 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
     CH_STAMP_DECL
     const int T = a.T;
     const double ecut = a.ecut;
-    // bounding box and finiteness in one pass; the four reductions interleaved
-    double xmn = __builtin_inf(), xmx = -__builtin_inf(), ymn = __builtin_inf(), ymx = -__builtin_inf();
-    bool finite = true;
-    for (int p = lane; p < N; p += 64) {
-        const double2 q = P[p];
-        xmn = fmin(xmn, q.x);
-        xmx = fmax(xmx, q.x);
-        ymn = fmin(ymn, q.y);
-        ymx = fmax(ymx, q.y);
-        finite = finite && (q.x - q.x == 0.0) && (q.y - q.y == 0.0);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double a0 = __shfl_xor(xmn, o), a1 = __shfl_xor(xmx, o), a2 = __shfl_xor(ymn, o), a3 = __shfl_xor(ymx, o);
-        xmn = fmin(xmn, a0);
-        xmx = fmax(xmx, a1);
-        ymn = fmin(ymn, a2);
-        ymx = fmax(ymx, a3);
-    }
-    const double bx = xmx - xmn, by = ymx - ymn;
-    const double E2 = unid((bx * bx + by * by) * (1.0 + 0x1p-20));
-    finite = finite && E2 < __builtin_inf();
-    if (N > 128 || ballot(!finite) != 0ull || !(ecut < __builtin_inf()))
+    const ChunkCut cc = chunk_cut(P, N, ecut, a.ecut_q, lane);
+    if (N > 128 || !cc.finite || !(ecut < __builtin_inf()))
         return chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack, cnt_out, lane);
 
     ChunkOut o;
@@ -537,15 +634,10 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
     o.n_inl = 0;
     o.last_inl = -1;
     o.n_draws = T + 1;
-    // Reassociated cross product r = fl(x uy - fl(y ux + k)) (two fmas),
-    // k = ox uy - oy ux per hypothesis, with the band widened by the
-    // R sqrt(ecut) term (see count_kernel) and tested as two cutoffs on |r|:
     // 2 FP64 ops + S + two counts per evaluation.  A lane whose counts differ (a point in the band)
     // or whose direction is not unit recounts exactly.
-    const double Rb = unid(fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx)));
-    const double margin = (E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
-    const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
-    const cut_t c_lo = count_cut(r_lo), c_hi = count_cut(r_hi);
+    const double margin = cc.margin;
+    const cut_t c_lo = cc.c_lo, c_hi = cc.c_hi;
     int M = 0;
     CH_STAMP(1);
     for (int tb = 0; tb < T; tb += 64) {
@@ -575,7 +667,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
             tsum[t] = exact_all ? -1.0 : S;  // negative: no bracket, always a candidate
             if (cnt_out) cnt_out[t] = c;
         }
-        M = max(M, wave_max(t < T ? c : 0));
+        M = max(M, wave_max_dpp(t < T ? c : 0));
     }
     M = uni(M);
     CH_STAMP(2);
@@ -599,7 +691,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
             double U = __builtin_inf();
             for (int k = lane; k < ntied; k += 64) {
                 const double S = tsum[tied[k]];
-                if (S >= 0.0) U = fmin(U, S + tie_bound_r(S, N, E2, Rb));
+                if (S >= 0.0) U = fmin(U, S + tie_bound_q(S, N, cc.tq));
             }
             U = wave_min_d(U);
             // a single candidate wins without its exact sum unless the stop test
@@ -610,7 +702,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
                 bool cand = false;
                 if (k < ntied) {
                     const double S = tsum[tied[k]];
-                    cand = S < 0.0 || S - tie_bound_r(S, N, E2, Rb) <= U;
+                    cand = S < 0.0 || S - tie_bound_q(S, N, cc.tq) <= U;
                 }
                 const uint64_t cm = ballot(cand);
                 if (cm && cand1 < 0) cand1 = kb + ffs64(cm);
@@ -625,7 +717,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
                 bool cand = false;
                 if (k < ntied) {
                     const double S = tsum[tied[k]];
-                    cand = S < 0.0 || S - tie_bound_r(S, N, E2, Rb) <= U;
+                    cand = S < 0.0 || S - tie_bound_q(S, N, cc.tq) <= U;
                 }
                 uint64_t cm = ballot(cand);
                 while (cm) {
@@ -2361,7 +2453,14 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
 }
 
 template <int HYP>
+#ifndef LSLAM_CHUNK_WAVES
+#define LSLAM_CHUNK_WAVES 0  // minimum waves per SIMD the allocation must allow (0: the compiler chooses; A/B)
+#endif
+#if LSLAM_CHUNK_WAVES > 0
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSLAM_CHUNK_WAVES))) void chunk_kernel(const KArgs a) {
+#else
 __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     WAVE_CENSUS(a, WC_CHUNK);
     if ((a.cons_prio >> 2) & 3) set_prio_level((a.cons_prio >> 2) & 3);
@@ -2515,10 +2614,11 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     // slack on it as on the E2 term.  Outside the band the cheap test decides
     // as before.
     const double Rb = fmax(fabs(xmn), fabs(xmx)) + fmax(fabs(ymn), fabs(ymx));
-    const double margin = (bx.E2 + ecut + Rb * (sqrt(ecut) * 1.01 + 1.0)) * 0x1p-42;
-    // c2 < ecut - margin  <=>  |r| <= r_lo;   c2 > ecut + margin  <=>  |r| >= r_hi
-    const double r_lo = sq_floor_lt(ecut - margin), r_hi = sq_ceil_gt(ecut + margin);
-    const cut_t c_lo = count_cut(r_lo), c_hi = count_cut(r_hi);
+    const double margin = (bx.E2 + ecut + Rb * a.ecut_q) * 0x1p-42;
+    // c2 < ecut - margin  <=  |r| below c_lo;   c2 > ecut + margin  <=  |r| above c_hi (cut_lo_of);
+    // only for a cheap chunk (the exact square-root search would not end for ecut = inf)
+    const cut_t c_lo = cheap ? cut_lo_of(ecut - margin) : count_cut(-1.0);
+    const cut_t c_hi = cheap ? cut_hi_of(ecut + margin) : count_cut(0.0);
     cdouble_t *mp = (cdouble_t *)(a.models + ((size_t)c * T + t0) * 4);
     const double nan = __builtin_nan("");
     if (cheap) {
@@ -3427,6 +3527,7 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         if (p->hyp_source == LSLAM_HYP_EXPLICIT && !b->hyp) return set_err(LSLAM_ERR_ARG, "explicit hyp without hyp");
         k.thr = p->residual_threshold;
         k.ecut = lslam_inlier_cutoff(p->residual_threshold);
+        k.ecut_q = std::sqrt(k.ecut) * 1.01 + 1.0;
         k.tol_a = p->tol_a;
         k.tol_b = p->tol_b;
         k.tol_dist = p->tol_dist;
