@@ -155,6 +155,7 @@ struct KArgs {
     int ep_d0, ep_nd;
     int ep_count;        // host: producer launches of the call
     size_t slot_jbytes;  // host: steps bytes of a slot (its MT state area follows)
+    int res_side;        // host: the resolve runs on the resolve stream (draws in the slot)
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     const uint8_t *spec_dirty_in;  // fix-up: scans whose speculative producer input was stale (replay)
     uint8_t *spec_dirty_out;       // fix-up: scans replayed by this call (the next call's dirty_in)
@@ -2950,11 +2951,18 @@ struct lslam_ctx {
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
     hipStream_t pstream;
-    void *pslot[2];
+    int nslots;                  // producer slots in the ring (LSLAM_SLOTS, 2 or 3)
+    void *pslot[3];
     size_t pslot_bytes;
     int next_slot;
-    hipEvent_t ev_slot_free[2];  // on stream, after the slot's resolve + fix-up
+    hipEvent_t ev_slot_free[3];  // on stream, after the slot's resolve + fix-up
     hipEvent_t ev_produced;      // on pstream, after rng_kernel
+    // The resolve of a one-launch producer runs on its own stream after the producer, off the
+    // ctx chain (LSLAM_RESOLVE_STREAM): its draws go to the slot, and the ctx stream waits for
+    // ev_resolved before the consensus.
+    int resolve_stream;
+    hipStream_t rstream;
+    hipEvent_t ev_resolved;      // on rstream, after the resolve
     hipEvent_t ev_copy;          // on stream, after the latest lslam_h2d / lslam_memset
     // destinations written by copies since the producer last waited for ev_copy: the producer
     // waits only if one of them is its input (seeds, CSR, MT state), so an xy upload per call
@@ -3114,7 +3122,12 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     }
     c->pstream = nullptr;
     c->ustream = nullptr;
-    c->pslot[0] = c->pslot[1] = nullptr;
+    c->rstream = nullptr;
+    c->pslot[0] = c->pslot[1] = c->pslot[2] = nullptr;
+    c->nslots = 2;
+    if (const char *e = getenv("LSLAM_SLOTS")) c->nslots = atoi(e) >= 3 ? 3 : 2;
+    c->resolve_stream = 0;
+    if (const char *e = getenv("LSLAM_RESOLVE_STREAM")) c->resolve_stream = atoi(e) != 0;
     c->pslot_bytes = 0;
     c->next_slot = 0;
     c->speculate = 1;
@@ -3152,15 +3165,15 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
         if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
         HIPCHK(hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, hi_pri));
     }
-    HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[0], hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[1], hipEventDisableTiming));
+    for (int i = 0; i < 3; i++) HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[i], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_resolved, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_ukf, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(c->ev_slot_free[0], c->stream));
-    HIPCHK(hipEventRecord(c->ev_slot_free[1], c->stream));
+    for (int i = 0; i < 3; i++) HIPCHK(hipEventRecord(c->ev_slot_free[i], c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     HIPCHK(hipEventRecord(c->ev_call, c->stream));
     {
@@ -3186,19 +3199,22 @@ int lslam_ctx_destroy(lslam_ctx *c) {
         }
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);
+    if (c->rstream) (void)hipStreamSynchronize(c->rstream);
     if (c->scr) (void)hipFree(c->scr);
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < 3; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
     if (c->rt_all) (void)hipFree(c->rt_all);
     for (int i = 0; i < 2; i++)
         if (c->spec_dirty[i]) (void)hipFree(c->spec_dirty[i]);
-    hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
+    hipEvent_t evs[8] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_slot_free[2], c->ev_produced,
+                         c->ev_copy,         c->ev_call,         c->ev_ukf,          c->ev_resolved};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
     if (c->pstream) (void)hipStreamDestroy(c->pstream);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
+    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -3209,6 +3225,7 @@ int lslam_sync(lslam_ctx *c) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->pstream));
     HIPCHK(hipStreamSynchronize(c->ustream));
+    HIPCHK(hipStreamSynchronize(c->rstream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return LSLAM_OK;
 }
@@ -3760,21 +3777,26 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     k.ep_d0 = 0;
     k.ep_count = (D + De - 1) / De;
     const size_t jbytes = ((size_t)De * per_draw + JBUF_FRONT + 64 + 255) & ~(size_t)255;
-    const size_t sbytes = (size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4;
-    if (c->pslot_bytes < jbytes + sbytes) {
+    const size_t sbytes = ((size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4 + 255) & ~(size_t)255;
+    // the resolve on its own stream (one launch): the draws live in the slot, so the next call's
+    // resolve does not overwrite the ones this call's consensus still reads
+    k.res_side = c->resolve_stream && !k.b.draws_out && k.ep_count == 1;
+    const size_t dbytes = k.res_side ? (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4 : 0;
+    if (c->pslot_bytes < jbytes + sbytes + dbytes) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipStreamSynchronize(c->pstream));
-        for (int i = 0; i < 2; i++) {
+        HIPCHK(hipStreamSynchronize(c->rstream));
+        for (int i = 0; i < 3; i++) {
             if (c->pslot[i]) HIPCHK(hipFree(c->pslot[i]));
             c->pslot[i] = nullptr;
         }
         c->pslot_bytes = 0;
-        for (int i = 0; i < 2; i++) {
-            hipError_t e = hipMalloc(&c->pslot[i], jbytes + sbytes);
+        for (int i = 0; i < c->nslots; i++) {
+            hipError_t e = hipMalloc(&c->pslot[i], jbytes + sbytes + dbytes);
             if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (producer slot)");
             HIPCHK(e);
         }
-        c->pslot_bytes = jbytes + sbytes;
+        c->pslot_bytes = jbytes + sbytes + dbytes;
         c->spec_ok = 0;  // the previous producer's end state went with the old slots
     }
     k.jbuf = (unsigned char *)c->pslot[slot] + JBUF_FRONT;
@@ -3782,6 +3804,8 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     k.slot_jbytes = jbytes;
     if (k.b.draws_out) {
         k.draws_scr = k.b.draws_out;
+    } else if (k.res_side) {
+        k.draws_scr = (int32_t *)((unsigned char *)c->pslot[slot] + jbytes + sbytes);
     } else {
         int st = ensure_scratch(c, (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4);
         if (st) return st;
@@ -3791,7 +3815,7 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
 }
 
 // resolve_kernel LDS: the chunk's staged steps (if they fit)
-static int launch_resolve(lslam_ctx *c, const KArgs &base) {
+static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     if (base.b.n_chunks == 0) return LSLAM_OK;
     KArgs k = base;
     const int N = k.b.max_chunk_points > 3 ? k.b.max_chunk_points : 3;
@@ -3807,8 +3831,8 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         // keep their residency (three per SIMD displaced them: C5 107 vs 78 ms per call)
         const int64_t cap = (k.ep_count > 1 && !c->epoch_serial) ? 8 * (int64_t)c->n_cus : (1 << 20);
         const dim3 grid(launch_cap(c, items > cap ? cap : items)), block(64);
-        if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, c->stream, k);
-        else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, c->stream, k);
+        if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, rs, k);
+        else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, rs, k);
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
@@ -3817,21 +3841,21 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         const int64_t items = (int64_t)k.b.n_chunks * ngroups;
         const dim3 grid(launch_cap(c, items > (1 << 30) ? (1 << 30) : items)), block(64);
         const int tl = 64 * (RB + 4) * esz;
-        if (k.j8) hipLaunchKernelGGL(resolve_big_kernel<uint8_t>, grid, block, tl, c->stream, k, ngroups);
-        else hipLaunchKernelGGL(resolve_big_kernel<uint16_t>, grid, block, tl, c->stream, k, ngroups);
+        if (k.j8) hipLaunchKernelGGL(resolve_big_kernel<uint8_t>, grid, block, tl, rs, k, ngroups);
+        else hipLaunchKernelGGL(resolve_big_kernel<uint16_t>, grid, block, tl, rs, k, ngroups);
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
     if (k.j8 && c->resolve_reg && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
         if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg == 3) {
             const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 127) / 128))), block(64);
-            hipLaunchKernelGGL(resolve_reg8x2_kernel, grid, block, 0, c->stream, k);
+            hipLaunchKernelGGL(resolve_reg8x2_kernel, grid, block, 0, rs, k);
         } else if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg != 2) {
             const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 63) / 64))), block(64);
-            hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, c->stream, k);
+            hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, rs, k);
         } else {
             const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
-            hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, c->stream, k);
+            hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, rs, k);
         }
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
@@ -3842,8 +3866,8 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base) {
         set_max_lds(resolve_kernel<uint16_t>);
     });
     const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
-    if (k.j8) hipLaunchKernelGGL(resolve_kernel<uint8_t>, grid, block, lds, c->stream, k);
-    else hipLaunchKernelGGL(resolve_kernel<uint16_t>, grid, block, lds, c->stream, k);
+    if (k.j8) hipLaunchKernelGGL(resolve_kernel<uint8_t>, grid, block, lds, rs, k);
+    else hipLaunchKernelGGL(resolve_kernel<uint16_t>, grid, block, lds, rs, k);
     HIPCHK(hipGetLastError());
     return LSLAM_OK;
 }
@@ -3919,16 +3943,27 @@ static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint3
         ke.b.mt_state_out = (last && final_out) ? final_out : ke.state_scr;
         int st = launch_rng(c, ke, ps);
         if (st) return st;
-        if (ps != c->stream) {
+        if (ps != c->stream && k.res_side) {
+            // resolve stream: after the producer, off the ctx chain; the ctx stream waits for it
+            // before the consensus
             HIPCHK(hipEventRecord(c->ev_produced, ps));
-            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
+            HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_produced, 0));
+            st = launch_resolve(c, ke, c->rstream);
+            if (st) return st;
+            HIPCHK(hipEventRecord(c->ev_resolved, c->rstream));
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_resolved, 0));
+        } else {
+            if (ps != c->stream) {
+                HIPCHK(hipEventRecord(c->ev_produced, ps));
+                HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
+            }
+            st = launch_resolve(c, ke, c->stream);
+            if (st) return st;
         }
-        st = launch_resolve(c, ke);
-        if (st) return st;
         if (!last) HIPCHK(hipEventRecord(c->ev_slot_free[sl], c->stream));
         prev_state = ke.state_scr;
         last_slot = sl;
-        sl ^= 1;
+        sl = (sl + 1) % c->nslots;
     }
     k.state_scr = const_cast<uint32_t *>(prev_state);
     c->next_slot = sl;
@@ -4170,7 +4205,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (mt) {
         st = prepare_steps(c, k, slot);
         if (st) return st;
-        c->next_slot ^= 1;
+        c->next_slot = (c->next_slot + 1) % c->nslots;
     }
     KArgs kp;
     int lds_post = 0;
@@ -4421,7 +4456,7 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     const int slot = c->next_slot;
     st = prepare_steps(c, k, slot);
     if (st) return st;
-    c->next_slot ^= 1;
+    c->next_slot = (c->next_slot + 1) % c->nslots;
     st = timer_begin(c, LSLAM_K_HYP);
     if (st) return st;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_slot_free[slot], 0));
