@@ -369,7 +369,18 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
 // random_interval's mask for step index i >= 1 (wave-uniform i: scalar ops)
 __device__ __forceinline__ uint32_t step_mask(uint32_t i) { return 0xffffffffu >> __clz((int)i); }
 
-__device__ __forceinline__ bool rt_rej(uint64_t M, uint32_t s) { return (int32_t)(uint32_t)((M << s) >> 32) < 0; }
+// LSLAM_REJ32=1: the sign test reads the shifted window's high dword only (an empty asm
+// keeps the compiler from folding it back into a 64-bit compare of the whole shift)
+#ifndef LSLAM_REJ32
+#define LSLAM_REJ32 0
+#endif
+__device__ __forceinline__ bool rt_rej(uint64_t M, uint32_t s) {
+    uint32_t hi = (uint32_t)((M << s) >> 32);
+#if LSLAM_REJ32
+    asm("" : "+v"(hi));
+#endif
+    return (int32_t)hi < 0;
+}
 
 // (sg + na) mod K for sg < K, na <= 64: one conditional subtraction when K >= 64
 // (KGE64, known at compile time: no per-window test of K)
