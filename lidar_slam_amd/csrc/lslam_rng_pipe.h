@@ -202,6 +202,22 @@ __device__ __forceinline__ uint32_t mbcnt_from(uint64_t m, uint32_t base) {
 // next draw boundary is d = (K-1 - sg - lane) + #rejected below the lane,
 // which v_mbcnt produces directly from R, and its Fisher-Yates index is
 // i = min(d, d+K) + 1 (unsigned; the window wraps past at most one boundary).
+// random_interval's mask for step index i >= 1 (wave-uniform i: scalar ops)
+__device__ __forceinline__ uint32_t step_mask(uint32_t i) { return 0xffffffffu >> __clz((int)i); }
+
+// tempered word & mask(K): the two xor-with-masked-shift steps as v_bitop3 ((a & b) ^ c)
+__device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
+    y ^= (y >> 11);
+    y = __builtin_amdgcn_bitop3_b32(y << 7, 0x9d2c5680u, y, 0x6a);
+    y = __builtin_amdgcn_bitop3_b32(y << 15, 0xefc60000u, y, 0x6a);
+    return (y ^ (y >> 18)) & mK;
+}
+
+// Mask-mode windows solved as a signed v_mbcnt test where the window stays in one draw and one
+// mask class (parse_chunk; A/B: LSLAM_MASK_LINEAR=0 keeps the 9-VALU evaluation everywhere)
+#ifndef LSLAM_MASK_LINEAR
+#define LSLAM_MASK_LINEAR 0
+#endif
 __device__ __forceinline__ uint32_t fy_index(uint32_t d, uint32_t K) { return min(d, d + K) + 1u; }
 __device__ __forceinline__ uint32_t fy_j(uint32_t w, uint32_t i) { return w & (0xffffffffu >> __clz((int)i)); }
 
@@ -277,9 +293,44 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 // next window's words: past the block's end this reads the rest of the pipe's LDS
                 // (the other block, the flags, the next pipe) or out-of-range zeros; never used
                 const uint32_t nraw = kb[pos + 64 + lane];
-                const uint32_t w = mt_temper(raw);
                 RP_STAMP(3);
                 const uint32_t b1 = K - 1u - sg;
+#if LSLAM_MASK_LINEAR
+                // Linear window: every step the window can reach, i = ihi - a for a <= 63, stays in
+                // the draw (b1 >= 63) and in one mask class m.  Lane l rejects iff (w & m) > ihi - a_l,
+                // a_l = l - (rejects below l), i.e. iff mbcnt(R, ihi - l - (w & m)) < 0 as a signed
+                // value: one evaluation is the two v_mbcnt and a compare (3 VALU instead of 9).
+                // C5's 4095-step draws: ~55 of a draw's ~64 windows.
+                {
+                    const uint32_t ihi = b1 + 1u;
+                    if (b1 >= 63u && step_mask(ihi) == step_mask(b1 - 62u)) {
+                        const uint32_t jv = rt_temper_mask(raw, step_mask(ihi));
+                        const uint32_t base = ihi - (uint32_t)lane - jv;
+                        uint64_t R = ballot((int32_t)(base + (uint32_t)lane - guess) < 0), Rp;  // a_l = guess
+#pragma unroll
+                        for (int e = 0; e < 2; e++) R = ballot((int32_t)mbcnt_from(R, base) < 0);
+                        uint32_t s;
+                        for (;;) {
+                            s = mbcnt_from(R, base);
+                            Rp = R;
+                            R = ballot((int32_t)s < 0);
+                            if (R == Rp) break;
+                        }
+                        RP_STAMP(2);
+                        RP_COUNT(5, 1);
+                        // a_l = l - (s - base) = ihi - jv - s
+                        store_accepted(J, g + (ihi - jv - s), jv, R);
+                        const uint32_t na = accepted_count(R);
+                        pos += 64;
+                        g += na;
+                        sg += na;
+                        if (sg >= K) sg -= K;
+                        raw = nraw;
+                        continue;
+                    }
+                }
+#endif
+                const uint32_t w = rt_temper_mask(raw, 0xffffffffu);
                 const uint32_t base0 = b1 - (uint32_t)lane;
                 uint32_t d = b1 - guess;
                 uint32_t i = fy_index(d, K);
@@ -366,8 +417,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
 // window M (x = sg + a) is its reject flag at that count, i.e. bit 63 of
 // M << s.  Accepted lanes store v at step g + a_l; the consumer applies
 // mask(i) itself (v & mask(i) = the step's j), so no per-lane i is formed here.
-// random_interval's mask for step index i >= 1 (wave-uniform i: scalar ops)
-__device__ __forceinline__ uint32_t step_mask(uint32_t i) { return 0xffffffffu >> __clz((int)i); }
 
 // LSLAM_REJ32=1: the sign test reads the shifted window's high dword only (an empty asm
 // keeps the compiler from folding it back into a 64-bit compare of the whole shift)
@@ -392,13 +441,6 @@ __device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
     return x;
 }
 
-// tempered word & mask(K): the two xor-with-masked-shift steps as v_bitop3 ((a & b) ^ c)
-__device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
-    y ^= (y >> 11);
-    y = __builtin_amdgcn_bitop3_b32(y << 7, 0x9d2c5680u, y, 0x6a);
-    y = __builtin_amdgcn_bitop3_b32(y << 15, 0xefc60000u, y, 0x6a);
-    return (y ^ (y >> 18)) & mK;
-}
 
 // evaluations after the first one before the first convergence check (tbl_window)
 #ifndef LSLAM_TBL_UNCHECKED
