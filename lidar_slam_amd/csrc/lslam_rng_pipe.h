@@ -213,11 +213,6 @@ __device__ __forceinline__ uint32_t rt_temper_mask(uint32_t y, uint32_t mK) {
     return (y ^ (y >> 18)) & mK;
 }
 
-// Mask-mode windows solved as a signed v_mbcnt test where the window stays in one draw and one
-// mask class (parse_chunk; A/B: LSLAM_MASK_LINEAR=0 keeps the 9-VALU evaluation everywhere)
-#ifndef LSLAM_MASK_LINEAR
-#define LSLAM_MASK_LINEAR 0
-#endif
 __device__ __forceinline__ uint32_t fy_index(uint32_t d, uint32_t K) { return min(d, d + K) + 1u; }
 __device__ __forceinline__ uint32_t fy_j(uint32_t w, uint32_t i) { return w & (0xffffffffu >> __clz((int)i)); }
 
@@ -295,45 +290,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 const uint32_t nraw = kb[pos + 64 + lane];
                 RP_STAMP(3);
                 const uint32_t b1 = K - 1u - sg;
-#if LSLAM_MASK_LINEAR
-                // Linear window: every step the window can reach, i = ihi - a for a <= 63, stays in
-                // the draw (b1 >= 63) and in one mask class m.  Lane l rejects iff (w & m) > ihi - a_l,
-                // a_l = l - (rejects below l), i.e. iff mbcnt(R, ihi - l - (w & m)) < 0 as a signed
-                // value: one evaluation is the two v_mbcnt and a compare (3 VALU instead of 9).
-                // C5's 4095-step draws: ~55 of a draw's ~64 windows.
-                {
-                    const uint32_t ihi = b1 + 1u;
-                    if (b1 >= 63u && step_mask(ihi) == step_mask(b1 - 62u)) {
-                        const uint32_t jv = rt_temper_mask(raw, step_mask(ihi));
-                        const uint32_t base = ihi - (uint32_t)lane - jv;
-                        uint64_t R = ballot((int32_t)(base + (uint32_t)lane - guess) < 0), Rp;  // a_l = guess
-                        // A lane decides the same at every a in [0, l] unless ihi - l < jv <= ihi,
-                        // i.e. ~base < l.  With no such lane (most windows of a long draw: P ~ e^(-2016/(m+1)))
-                        // the guess is the fixed point: no ballot round trip to confirm it.
-                        const uint64_t sens = ballot(~base < (uint32_t)lane);
-                        uint32_t s = mbcnt_from(R, base);
-                        if (sens != 0) {
-                            for (;;) {
-                                Rp = R;
-                                R = ballot((int32_t)s < 0);
-                                if (R == Rp) break;
-                                s = mbcnt_from(R, base);
-                            }
-                        }
-                        RP_STAMP(2);
-                        RP_COUNT(5, 1);
-                        // a_l = l - (s - base) = ihi - jv - s
-                        store_accepted(J, g + (ihi - jv - s), jv, R);
-                        const uint32_t na = accepted_count(R);
-                        pos += 64;
-                        g += na;
-                        sg += na;
-                        if (sg >= K) sg -= K;
-                        raw = nraw;
-                        continue;
-                    }
-                }
-#endif
                 const uint32_t w = rt_temper_mask(raw, 0xffffffffu);
                 const uint32_t base0 = b1 - (uint32_t)lane;
                 uint32_t d = b1 - guess;
