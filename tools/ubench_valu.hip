@@ -12,11 +12,11 @@
 
 #define ITER 256
 
-enum Op { XOR32 = 0, MBCNT, LSHL64, CMP64, CMP32, BITOP3, ALIGNBIT, EVAL64, EVAL32, FMA64, NOPS };
+enum Op { XOR32 = 0, MBCNT, LSHL64, CMP64, CMP32, BITOP3, ALIGNBIT, EVAL64, EVAL32, FMA64, XOR64E, CMPE32, CMPE64ND, MAD24, NOPS };
 static const char *names[NOPS] = {"v_xor_b32", "v_mbcnt_lo+hi (pair)", "v_lshlrev_b64", "v_cmp_gt_i64_e64",
                                   "v_cmp_gt_i32_e64", "v_bitop3_b32", "v_alignbit_b32",
                                   "eval: mbcnt x2 + lshl_b64 + cmp_i64 (dependent)",
-                                  "eval: mbcnt x2 + lshl_b64 + cmp_i32 hi (dependent)", "v_fma_f64"};
+                                  "eval: mbcnt x2 + lshl_b64 + cmp_i32 hi (dependent)", "v_fma_f64", "v_xor_b32_e64 (VOP3 encoding)", "v_cmp_gt_i32_e32 (vcc, no consumer)", "v_cmp_gt_i32_e64 (sgpr, no consumer)", "v_mad_u32_u24"};
 
 template <int OP, bool DEP>
 __global__ void kern(uint64_t *out, uint32_t seed) {
@@ -83,6 +83,21 @@ __global__ void kern(uint64_t *out, uint32_t seed) {
                     asm volatile("v_cmp_gt_i32_e64 %0, 0, %1" : "=s"(R[k]) : "v"((uint32_t)(sh >> 32)));
             }
             s0 = R[0] ^ R[1] ^ R[2] ^ R[3];
+        } else if (OP == XOR64E) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) asm volatile("v_xor_b32_e64 %0, %1, %0" : "+v"(a[k]) : "v"(b[k]));
+        } else if (OP == CMPE32) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) asm volatile("v_cmp_gt_i32_e32 vcc, 0, %0" ::"v"(a[k]) : "vcc");
+        } else if (OP == CMPE64ND) {
+            uint64_t r0, r1, r2, r3;
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                asm volatile("v_cmp_gt_i32_e64 %0, 0, %4\n\tv_cmp_gt_i32_e64 %1, 0, %5\n\tv_cmp_gt_i32_e64 %2, 0, %6\n\tv_cmp_gt_i32_e64 %3, 0, %7"
+                             : "=s"(r0), "=s"(r1), "=s"(r2), "=s"(r3) : "v"(a[4 * k]), "v"(a[4 * k + 1]), "v"(a[4 * k + 2]), "v"(a[4 * k + 3]));
+        } else if (OP == MAD24) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) asm volatile("v_mad_u32_u24 %0, %1, 28, %0" : "+v"(a[k]) : "v"(b[k]));
         } else if (OP == FMA64) {
 #pragma unroll
             for (int k = 0; k < 8; k++) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(f[k]) : "v"(DEP ? f[k] : 1.0));
@@ -138,6 +153,10 @@ int main() {
     one<EVAL64>(d, h, false);
     one<EVAL32>(d, h, false);
     one<FMA64>(d, h, false);
+    one<XOR64E>(d, h, false);
+    one<CMPE32>(d, h, false);
+    one<CMPE64ND>(d, h, false);
+    one<MAD24>(d, h, false);
     printf("}\n");
     hipFree(d);
     return 0;
