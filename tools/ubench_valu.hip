@@ -12,11 +12,11 @@
 
 #define ITER 256
 
-enum Op { XOR32 = 0, MBCNT, LSHL64, CMP64, CMP32, BITOP3, ALIGNBIT, EVAL64, EVAL32, FMA64, XOR64E, CMPE32, CMPE64ND, MAD24, NOPS };
+enum Op { XOR32 = 0, MBCNT, LSHL64, CMP64, CMP32, BITOP3, ALIGNBIT, EVAL64, EVAL32, FMA64, XOR64E, CMPE32, CMPE64ND, MAD24, SADD, MIX, NOPS };
 static const char *names[NOPS] = {"v_xor_b32", "v_mbcnt_lo+hi (pair)", "v_lshlrev_b64", "v_cmp_gt_i64_e64",
                                   "v_cmp_gt_i32_e64", "v_bitop3_b32", "v_alignbit_b32",
                                   "eval: mbcnt x2 + lshl_b64 + cmp_i64 (dependent)",
-                                  "eval: mbcnt x2 + lshl_b64 + cmp_i32 hi (dependent)", "v_fma_f64", "v_xor_b32_e64 (VOP3 encoding)", "v_cmp_gt_i32_e32 (vcc, no consumer)", "v_cmp_gt_i32_e64 (sgpr, no consumer)", "v_mad_u32_u24"};
+                                  "eval: mbcnt x2 + lshl_b64 + cmp_i32 hi (dependent)", "v_fma_f64", "v_xor_b32_e64 (VOP3 encoding)", "v_cmp_gt_i32_e32 (vcc, no consumer)", "v_cmp_gt_i32_e64 (sgpr, no consumer)", "v_mad_u32_u24", "s_add_u32 (SALU; per_simd_Nw = per SIMD share, x4 for per CU)", "mix: 8 v_xor_b32 + 8 s_add_u32 per iteration (per_simd: cycles per xor+s_add pair)"};
 
 template <int OP, bool DEP>
 __global__ void kern(uint64_t *out, uint32_t seed) {
@@ -98,6 +98,27 @@ __global__ void kern(uint64_t *out, uint32_t seed) {
         } else if (OP == MAD24) {
 #pragma unroll
             for (int k = 0; k < 8; k++) asm volatile("v_mad_u32_u24 %0, %1, 28, %0" : "+v"(a[k]) : "v"(b[k]));
+        } else if (OP == SADD) {
+            uint32_t q0 = (uint32_t)s0, q1 = (uint32_t)s1, q2 = q0 ^ 5u, q3 = q1 ^ 7u, q4 = q0 + 3u, q5 = q1 + 9u,
+                     q6 = q0 * 3u, q7 = q1 * 5u;
+            asm volatile(
+                "s_add_u32 %0, %0, 3\n\ts_add_u32 %1, %1, 5\n\ts_add_u32 %2, %2, 7\n\ts_add_u32 %3, %3, 9\n\t"
+                "s_add_u32 %4, %4, 3\n\ts_add_u32 %5, %5, 5\n\ts_add_u32 %6, %6, 7\n\ts_add_u32 %7, %7, 9"
+                : "+s"(q0), "+s"(q1), "+s"(q2), "+s"(q3), "+s"(q4), "+s"(q5), "+s"(q6), "+s"(q7)::"scc");
+            s0 = (uint64_t)(q0 ^ q1 ^ q2 ^ q3) << 32 | (q4 ^ q5 ^ q6 ^ q7);
+        } else if (OP == MIX) {
+            uint32_t q0 = (uint32_t)s0, q1 = (uint32_t)s1, q2 = q0 ^ 5u, q3 = q1 ^ 7u, q4 = q0 + 3u, q5 = q1 + 9u,
+                     q6 = q0 * 3u, q7 = q1 * 5u;
+            asm volatile(
+                "s_add_u32 %0, %0, 3\n\tv_xor_b32 %8, %16, %8\n\ts_add_u32 %1, %1, 5\n\tv_xor_b32 %9, %16, %9\n\t"
+                "s_add_u32 %2, %2, 7\n\tv_xor_b32 %10, %16, %10\n\ts_add_u32 %3, %3, 9\n\tv_xor_b32 %11, %16, %11\n\t"
+                "s_add_u32 %4, %4, 3\n\tv_xor_b32 %12, %16, %12\n\ts_add_u32 %5, %5, 5\n\tv_xor_b32 %13, %16, %13\n\t"
+                "s_add_u32 %6, %6, 7\n\tv_xor_b32 %14, %16, %14\n\ts_add_u32 %7, %7, 9\n\tv_xor_b32 %15, %16, %15"
+                : "+s"(q0), "+s"(q1), "+s"(q2), "+s"(q3), "+s"(q4), "+s"(q5), "+s"(q6), "+s"(q7),
+                  "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                : "v"(b[0])
+                : "scc");
+            s0 = (uint64_t)(q0 ^ q1 ^ q2 ^ q3) << 32 | (q4 ^ q5 ^ q6 ^ q7);
         } else if (OP == FMA64) {
 #pragma unroll
             for (int k = 0; k < 8; k++) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(f[k]) : "v"(DEP ? f[k] : 1.0));
@@ -126,6 +147,8 @@ static double run(int W, uint64_t *d_out, std::vector<uint64_t> &h) {
     // wave-instructions per wave in the loop
     double per = 8.0;
     if (OP == MBCNT) per = 16.0;
+    if (OP == SADD) per = 77.0 / 4.0;
+    if (OP == MIX) per = 8.0;  // pairs (plus ~11 combining SALU per iteration, see SADD)  // SALU instructions per iteration in the compiled loop (4 iterations: 77)
     if (OP == EVAL64 || OP == EVAL32) per = (DEP ? 1.0 : 4.0) * 4.0;
     // cycles per wave-instruction per SIMD (W/4 waves per SIMD share it)
     return med / (ITER * per) / (W >= 4 ? W / 4.0 : 1.0);
@@ -157,6 +180,8 @@ int main() {
     one<CMPE32>(d, h, false);
     one<CMPE64ND>(d, h, false);
     one<MAD24>(d, h, false);
+    one<SADD>(d, h, false);
+    one<MIX>(d, h, false);
     printf("}\n");
     hipFree(d);
     return 0;
