@@ -407,6 +407,9 @@ __device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
 #ifndef LSLAM_TBL_UNCHECKED
 #define LSLAM_TBL_UNCHECKED 2
 #endif
+#ifndef LSLAM_TBL_ASM
+#define LSLAM_TBL_ASM 1  // a table window's evaluations, checked turns and store as one asm block (0: the compiler's form, A/B)
+#endif
 
 typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
 __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
@@ -478,6 +481,69 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     // 0.777 vs 0.793 ms with three): the producer's VALU count, not its checks' latency, is what
     // the consumers beside it feel.  A count-based test (converged when mbcnt(R) repeats the
     // counts, which needs no confirming evaluation) was slower: 6 VALU per checked turn.
+#if LSLAM_TBL_ASM && LSLAM_TBL_UNCHECKED == 2 && LSLAM_REJ32 && !defined(LSLAM_STAMPS) && !defined(LSLAM_TBL_LATECHECK)
+    // The evaluations, the checked turns and the store as one asm block: the checked turns keep
+    // the ballot in VCC and in s[40:41] in turn, so no turn copies the ballot it compares against
+    // (the compiler's loop spends an s_mov_b64 per turn).  Wait states: one between the 64-bit
+    // shift and the compare of its high dword, two between a compare's mask and the v_mbcnt that
+    // reads it (an s_nop 1, or the s_cmp + s_cbranch of a turn).  Both exits leave the fixed
+    // point in VCC (equal to s[40:41]) and its counts in S.  v[28:29] is the shift's scratch pair.
+    uint32_t na, tS, tI;
+    uint64_t tE;
+#define TBL_EVAL_VCC                                \
+    "v_mbcnt_lo_u32_b32 %[S], vcc_lo, %[sb]\n\t"  \
+    "v_mbcnt_hi_u32_b32 %[S], vcc_hi, %[S]\n\t"   \
+    "v_lshlrev_b64 v[28:29], %[S], %[M]\n\t"      \
+    "s_nop 0\n\t"                                 \
+    "v_cmp_gt_i32_e32 vcc, 0, v29\n\t"            \
+    "s_nop 1\n\t"
+#define TBL_TURNS                                                   \
+    "v_lshlrev_b64 v[28:29], %[s0], %[M]\n\t"                     \
+    "s_nop 0\n\t"                                                 \
+    "v_cmp_gt_i32_e32 vcc, 0, v29\n\t"                            \
+    "s_nop 1\n\t" TBL_EVAL_VCC TBL_EVAL_VCC                        \
+    "TBLA_%=:\n\t"                                            \
+    "v_mbcnt_lo_u32_b32 %[S], vcc_lo, %[sb]\n\t"                  \
+    "v_mbcnt_hi_u32_b32 %[S], vcc_hi, %[S]\n\t"                   \
+    "v_lshlrev_b64 v[28:29], %[S], %[M]\n\t"                      \
+    "s_nop 0\n\t"                                                 \
+    "v_cmp_gt_i32_e64 s[40:41], 0, v29\n\t"                       \
+    "s_cmp_eq_u64 s[40:41], vcc\n\t"                              \
+    "s_cbranch_scc1 TBLX_%=\n\t"                              \
+    "v_mbcnt_lo_u32_b32 %[S], s40, %[sb]\n\t"                     \
+    "v_mbcnt_hi_u32_b32 %[S], s41, %[S]\n\t"                      \
+    "v_lshlrev_b64 v[28:29], %[S], %[M]\n\t"                      \
+    "s_nop 0\n\t"                                                 \
+    "v_cmp_gt_i32_e32 vcc, 0, v29\n\t"                            \
+    "s_cmp_eq_u64 vcc, s[40:41]\n\t"                              \
+    "s_cbranch_scc0 TBLA_%=\n"                                 \
+    "TBLX_%=:\n\t"                                            \
+    "v_sub_u32 %[I], %[gq], %[S]\n\t"
+    if constexpr (sizeof(JT) == 1) {
+        asm volatile(TBL_TURNS
+                     "s_andn1_saveexec_b64 %[E], vcc\n\t"
+                     "global_store_byte %[I], %[v], %[J]\n\t"
+                     "s_mov_b64 exec, %[E]\n\t"
+                     "s_bcnt0_i32_b64 %[na], vcc\n\t"
+                     "s_nop 0"
+                     : [na] "=s"(na), [S] "=&v"(tS), [I] "=&v"(tI), [E] "=&s"(tE)
+                     : [M] "v"(M), [s0] "v"(s0), [sb] "v"(sbase), [v] "v"(v), [gq] "s"(gq), [J] "s"(J)
+                     : "vcc", "scc", "v28", "v29", "s40", "s41", "memory");
+    } else {
+        asm volatile(TBL_TURNS
+                     "v_lshlrev_b32 %[I], 1, %[I]\n\t"
+                     "s_andn1_saveexec_b64 %[E], vcc\n\t"
+                     "global_store_short %[I], %[v], %[J]\n\t"
+                     "s_mov_b64 exec, %[E]\n\t"
+                     "s_bcnt0_i32_b64 %[na], vcc\n\t"
+                     "s_nop 0"
+                     : [na] "=s"(na), [S] "=&v"(tS), [I] "=&v"(tI), [E] "=&s"(tE)
+                     : [M] "v"(M), [s0] "v"(s0), [sb] "v"(sbase), [v] "v"(v), [gq] "s"(gq), [J] "s"(J)
+                     : "vcc", "scc", "v28", "v29", "s40", "s41", "memory");
+    }
+#undef TBL_TURNS
+#undef TBL_EVAL_VCC
+#else
     uint64_t R = ballot(rt_rej(M, s0));
 #pragma unroll
     for (int e = 0; e < LSLAM_TBL_UNCHECKED; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
@@ -528,6 +594,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     WSTAMP(3);
     store_accepted(J, gq - s, v, R);
     const uint32_t na = accepted_count(R);
+#endif
     pos += 64;
     gq += na;
     sg = rt_wrap<KGE64>(sg + na, K);
