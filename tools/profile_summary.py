@@ -105,6 +105,23 @@ def main(tag, bench_log=None):
         for k, d in sq.items():
             for n, v in d.items():
                 lines.append("| `%s` | %s | %.4g | %.4g |" % (k, n, v, v / scans))
+        # Issue view of the whole step: wave-instructions per scan over every kernel,
+        # per SIMD per step (4 scans per SIMD at 4096 scans on 1024 SIMDs), and the cycles per
+        # instruction that leaves at the producer's own clock (SQ_WAVE_CYCLES are quad-cycles).
+        kinds = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_INSTS_SMEM")
+        tot = sum(d.get(n, 0.0) for d in sq.values() for n in kinds) / scans
+        rng = sq.get("rng_kernel", {})
+        roc = [float(r["AverageNs"]) / 1e3 for r in stats if "rng_kernel" in r["Name"]]
+        if tot and rng.get("SQ_WAVE_CYCLES") and roc:
+            ghz = 4.0 * rng["SQ_WAVE_CYCLES"] / scans / (roc[0] * 1e3)
+            simds = 1024.0
+            per_simd = tot * scans / simds
+            step_cyc = bench["ms_per_step"] * 1e6 * ghz
+            lines += ["", "Issue: %.0f wave-instructions per scan (VALU + SALU + branch + LDS + SMEM, all kernels), "
+                      "%.0f per SIMD per step; at the producer's clock under the profiler (%.2f GHz: SQ_WAVE_CYCLES x 4 "
+                      "per wave / rocprof average) the bench line's %.4f ms step is %.0f cycles = %.2f cycles per "
+                      "instruction per SIMD (micro-benchmark: 2.0 for simple ops, 3.3 for v_bitop3/v_mbcnt/64-bit ops)."
+                      % (tot, per_simd, ghz, bench["ms_per_step"], step_cyc, step_cyc / per_simd)]
     prof_line = [l for l in open(os.path.join(S, "kt.log")) if l.startswith('{"metric"')]
     if prof_line:
         pb = json.loads(prof_line[-1])
