@@ -66,8 +66,9 @@ enum {
     LSLAM_NEW_LANDMARK = 64,  /* no landmark matched: the chunk's Landmark was appended */
     LSLAM_MATCHED = 128,      /* an existing landmark matched (its life reset to LIFE) */
     LSLAM_CAPACITY = 256,     /* no match and the list was full: the new landmark was dropped */
-    LSLAM_CHUNK_BOUND = 512   /* the scan has more chunks than lslam_scan_batch.max_scan_chunks declared
-                                 (a hard bound for the staged post passes): not associated */
+    LSLAM_CHUNK_BOUND = 512   /* LSLAM_UKF_MAP only: a matched chunk at index >= max_scan_chunks of its
+                                 scan (an understated max_scan_chunks) has no measurement slot, so the
+                                 UKF update does not use it; association and outputs are unaffected */
 };
 
 /* ---- hypothesis sources ---- */
@@ -158,8 +159,10 @@ typedef struct lslam_scan_batch {
     int32_t n_chunks;               /* = scan_chunk_off[n_scans] */
     int64_t n_points;               /* = chunk_pt_off[n_chunks] */
     int32_t max_chunk_points;       /* max chunk size N over the batch */
-    int32_t max_scan_chunks;        /* max chunks per scan: a hard bound (LDS is sized by it; a scan with
-                                       more chunks is flagged LSLAM_CHUNK_BOUND by the association) */
+    int32_t max_scan_chunks;        /* max chunks per scan: sizes the post pass's LDS staging.  A scan with
+                                       more chunks gets the same results through the unstaged paths (a
+                                       rewind snapshot per chunk, records walked in place); only
+                                       LSLAM_UKF_MAP's measurement slots stop there (LSLAM_CHUNK_BOUND) */
     int32_t lmk_capacity;           /* per-scan landmark list capacity */
     int32_t reserved;
     /* inputs */

@@ -103,11 +103,7 @@ __device__ __forceinline__ int owning_scan(const lslam_scan_batch &B, int c) {
 enum { MODE_RANSAC = 1, MODE_ASSOC = 2, MODE_UKF = 4, MODE_HYP_ONLY = 8, MODE_POST = 16 };
 
 // A chunk's bounding-box terms and residual cutoffs (chunk_consensus, cut_finish).
-#ifndef LSLAM_COUNT_F64CMP
 typedef float cut_t;  // the count loops' cutoffs: FP32 on the residual's high dword (count_one)
-#else
-typedef double cut_t;
-#endif
 struct ChunkCut {
     double tq;      // tie brackets: an upper bound of E2 + R (sqrt(E2) + 1) (tie_bound_q)
     double margin;  // the exact-test band around ecut
@@ -131,7 +127,7 @@ struct KArgs {
     int life;
     // LDS layout (byte offsets into dynamic shared memory)
     int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum, off_inl;
-    int off_vstack, off_nstack, off_hist, off_lmk, off_vis, off_mask, off_corg, off_zobs;
+    int off_vstack, off_nstack, off_snap, off_lmk, off_vis, off_mask, off_corg, off_zobs;
     int corg_cap;
     int off_recs;       // post pass: the scan's chunk records + chunk offsets (-1: per-chunk loop)
     int off_ukf;
@@ -146,20 +142,18 @@ struct KArgs {
     int res_g;          // resolve_kernel: LDS staging capacity (bytes)
     int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
     uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
-    int off_blk, off_fl, off_nxt, off_vtmp, off_stage, off_tbl;
+    int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
-    int off_stbl;        // rng_kernel, shared tables (>= 0): [2] K claims then 2 tables after the pipes
-    const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127 (null: mask evaluation only)
+    int off_stbl;        // rng_kernel: [2] K claims then 2 shared reject tables, after the pipes
+    const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127
     // producer epochs (one-chunk scans whose steps exceed the slot budget): this launch
     // covers draws [ep_d0, ep_d0 + ep_nd) of every chunk; ep_nd = 0: all T + 1 draws
     int ep_d0, ep_nd;
     int ep_count;        // host: producer launches of the call
     size_t slot_jbytes;  // host: steps bytes of a slot (its MT state area follows)
-    int res_side;        // host: the resolve runs on the resolve stream (draws in the slot)
     int fixup;          // scan_kernel: only scans with an early-stopped chunk run
     const uint8_t *spec_dirty_in;  // fix-up: scans whose speculative producer input was stale (replay)
     uint8_t *spec_dirty_out;       // fix-up: scans replayed by this call (the next call's dirty_in)
-    int cons_prio;      // wave priority of the consumer kernels: resolve | chunk << 2 | post << 4
     int write_yproj;    // chunk_kernel: y_proj with the chunk's own line (no association pass)
     int lmk_reg;        // post pass (association only, lmk_cap <= 64): landmark list in registers
     // large chunks (N > 128): count_kernel -> select_kernel
@@ -417,7 +411,6 @@ __device__ __forceinline__ double sd(unsigned lo, unsigned hi) {
 
 // one point against the lane's hypothesis: r = fl(x uy - fl(y ux + k)),
 // S += r^2, lo += |r| <= r_lo, hi += |r| < r_hi
-#ifndef LSLAM_COUNT_F64CMP
 // The two cutoffs are tested on r's HIGH dword read as a float (sign, exponent and the top 20
 // mantissa bits of the double; for non-negative values its order is the double's): the sure
 // inliers are |hi(r)| < hi(r_lo) (so |r| < r_lo), the possible ones |hi(r)| <= hi(r_hi) (every
@@ -439,19 +432,6 @@ __device__ __forceinline__ void count_one(double x, double y, double ux, double 
     hi += maybe_in(r, c_hi) ? 1 : 0;
     asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
 }
-#else
-__device__ __forceinline__ cut_t count_cut(double c) { return c; }
-__device__ __forceinline__ bool sure_in(double r, cut_t c) { return fabs(r) <= c; }
-__device__ __forceinline__ bool maybe_in(double r, cut_t c) { return fabs(r) < c; }
-__device__ __forceinline__ void count_one(double x, double y, double ux, double uy, double k, double r_lo,
-                                          double r_hi, int &lo, int &hi, double &S) {
-    const double r = __builtin_fma(x, uy, -__builtin_fma(y, ux, k));
-    S = __builtin_fma(r, r, S);
-    lo += sure_in(r, r_lo) ? 1 : 0;
-    hi += maybe_in(r, r_hi) ? 1 : 0;
-    asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
-}
-#endif
 
 // one hypothesis per lane against all N points (gP: global, wave-uniform)
 __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, double ux, double uy, double k,
@@ -576,16 +556,12 @@ __device__ __forceinline__ float hi_units(double s, int d) {
     return __uint_as_float((uint32_t)(__double_as_longlong(s) >> 32) + (uint32_t)d);
 }
 __device__ __forceinline__ cut_t cut_lo_of(double e) {
-#ifndef LSLAM_COUNT_F64CMP
     if (!(e > 0.0)) return -1.0f;
     if (e >= 0x1p-100 && e <= 0x1p100) return hi_units((double)__builtin_amdgcn_sqrtf((float)e), -2);
-#endif
     return count_cut(sq_floor_lt(e));
 }
 __device__ __forceinline__ cut_t cut_hi_of(double e) {
-#ifndef LSLAM_COUNT_F64CMP
     if (e >= 0x1p-100 && e <= 0x1p100) return hi_units((double)__builtin_amdgcn_sqrtf((float)e), 2);
-#endif
     return count_cut(sq_ceil_gt(e));
 }
 
@@ -1164,13 +1140,16 @@ __device__ int associate_reg(const KArgs &ka, LmkReg &e, int &L, double a, doubl
     return match;
 }
 
-__device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, int lane) {
+// staged: the scan's chunk records and offsets are copied into rbuf (LDS, max_scan_chunks =
+// hist_cap records) and back; a scan with more chunks than the batch declared walks its records
+// in place (HBM) and writes y_proj chunk by chunk: the same results, one extra load per record.
+__device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool staged, int lane) {
     const lslam_scan_batch &B = a.b;
     const int c0 = B.scan_chunk_off[s], nchunks = B.scan_chunk_off[s + 1] - c0;
     const int id0 = B.id_base ? B.id_base[s] : 0;
-    lslam_chunk_model *recs = (lslam_chunk_model *)rbuf;
+    lslam_chunk_model *recs = staged ? (lslam_chunk_model *)rbuf : B.models + c0;
     int32_t *off = (int32_t *)(rbuf + (((int)sizeof(lslam_chunk_model) * a.hist_cap + 15) & ~15));
-    {
+    if (staged) {
         const uint4 *src = (const uint4 *)(B.models + c0);
         uint4 *dst = (uint4 *)rbuf;
         for (int e = lane; e < nchunks * 7; e += 64) dst[e] = src[e];
@@ -1206,6 +1185,14 @@ __device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, int l
         }
         __syncthreads();  // every lane has its copy of recs[ci]
         if (lane == 0) recs[ci] = rec;
+        if (!staged && B.y_proj) {
+            const int q0 = B.chunk_pt_off[c0 + ci], q1 = B.chunk_pt_off[c0 + ci + 1];
+            const bool have_model = (rec.flags & LSLAM_VALID) != 0;
+            for (int q = q0 + lane; q < q1; q += 64) {
+                const double x = B.xy ? B.xy[2 * (size_t)q] : polar_xy(B.theta_deg[q], B.dist_mm[q]).x;
+                B.y_proj[q] = (have_model && B.inlier_mask[q]) ? (rec.proj_a * x + rec.proj_b) : 0.0;
+            }
+        }
     }
     if (lane < L) {
         lslam_landmark g;
@@ -1214,6 +1201,7 @@ __device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, int l
         lst[lane] = g;
     }
     if (lane == 0) B.lmk_count[s] = L;
+    if (!staged) return;
     __syncthreads();
     {
         const uint4 *src = (const uint4 *)rbuf;
@@ -1267,7 +1255,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
     uint8_t *mk = (uint8_t *)(smem + a.off_mask);
     double *vstack = (double *)(smem + a.off_vstack);
     int *nstack = (int *)(smem + a.off_nstack);
-    int32_t *hist = (int32_t *)(smem + a.off_hist);
+    uint32_t *snap = (uint32_t *)(smem + a.off_snap);  // MT state at the current chunk's start (rewind)
     double2 *corg = (double2 *)(smem + a.off_corg);
     double2 *zobs = (double2 *)(smem + a.off_zobs);
     lslam_landmark *lmk = (lslam_landmark *)(smem + a.off_lmk);
@@ -1323,17 +1311,13 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
     if (use_mt) mt_init();
 
     // the staged post passes hold the scan's chunk records in an LDS area of max_scan_chunks
-    // (hist_cap) records: a scan with more chunks than the batch declared takes the per-chunk
-    // loop below, or, with the register list (which has no LDS list to fall back on), is
-    // flagged LSLAM_CHUNK_BOUND and left unassociated
+    // (hist_cap) records: a scan with more chunks than the batch declared walks them in place
+    // (post_assoc_reg) or takes the per-chunk loop below, with the same results
+    // (test_gpu_bounds.py); only map mode's measurement slots end there (LSLAM_CHUNK_BOUND)
     const bool recs_fit = nchunks <= a.hist_cap;
     if constexpr (kPost && (MODE & MODE_ASSOC) != 0 && (MODE & MODE_UKF) == 0) {
         if (a.lmk_reg) {  // the list in registers (association-only post pass, lmk_cap <= 64)
-            if (!recs_fit) {
-                for (int c = c0 + lane; c < c1; c += 64) B.models[c].flags |= LSLAM_CHUNK_BOUND;
-                return;
-            }
-            post_assoc_reg(a, s, smem + a.off_recs, lane);
+            post_assoc_reg(a, s, smem + a.off_recs, recs_fit, lane);
             return;
         }
     }
@@ -1400,12 +1384,17 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                     if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
                     if (B.y_proj) B.y_proj[p0 + p] = 0.0;
                 }
-                if (use_mt && ci < a.hist_cap && lane == 0) hist[ci] = 0;
                 __syncthreads();
                 continue;
             }
             // ---- A3: draws
             const int D = T + 1;
+            int snap_pos = 0;
+            if (use_mt && !(MODE & MODE_HYP_ONLY)) {  // the stream at the chunk's start, for an early stop
+                for (int i = lane; i < MT_N; i += 64) snap[i] = key[i];
+                snap_pos = mt.pos;
+                __syncthreads();
+            }
             if (HYP == LSLAM_HYP_MT19937) {
                 mt_draws(mt, (uint32_t)N, (uint32_t)D, draws, true, lane);
             } else if (HYP == LSLAM_HYP_PHILOX) {
@@ -1420,7 +1409,6 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 for (int i = lane; i < 2 * D; i += 64) dst[i] = draws[i];
             }
             if (MODE & MODE_HYP_ONLY) {
-                if (use_mt && ci < a.hist_cap && lane == 0) hist[ci] = D;
                 __syncthreads();
                 continue;
             }
@@ -1430,19 +1418,14 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
             // ---- A4-A7
             const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack,
                                             B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
-            if (use_mt) {
-                if (ci < a.hist_cap && lane == 0) hist[ci] = o.n_draws;
+            if (use_mt && o.n_draws < D) {
+                // early stop: rewind the stream to the chunk's start, then exactly o.n_draws draws
+                // (the snapshot holds any number of chunks: max_scan_chunks does not bound it)
                 __syncthreads();
-                if (o.n_draws < D) {
-                    // early stop: rewind the stream to exactly o.n_draws draws into this chunk
-                    mt_init();
-                    for (int cj = 0; cj < ci && cj < a.hist_cap; cj++) {
-                        const int nj = B.chunk_pt_off[c0 + cj + 1] - B.chunk_pt_off[c0 + cj];
-                        const int dj = uni(hist[cj]);
-                        if (nj >= 3 && dj > 0) mt_draws(mt, (uint32_t)nj, (uint32_t)dj, nullptr, false, lane);
-                    }
-                    mt_draws(mt, (uint32_t)N, (uint32_t)o.n_draws, nullptr, false, lane);
-                }
+                for (int i = lane; i < MT_N; i += 64) key[i] = snap[i];
+                mt.pos = snap_pos;
+                __syncthreads();
+                mt_draws(mt, (uint32_t)N, (uint32_t)o.n_draws, nullptr, false, lane);
             }
             have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
             if (have_model && ci < a.corg_cap && lane == 0) corg[ci] = make_double2(rec.ox, rec.oy);
@@ -1475,6 +1458,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 rec.match_index = m;
                 rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
                 if (overflow) rec.flags |= LSLAM_CAPACITY;
+                if (m >= 0 && ci >= a.corg_cap) rec.flags |= LSLAM_CHUNK_BOUND;  // no measurement slot
                 if (m >= 0 && ci < a.corg_cap) {
                     // measurement of map landmark m (hx = range/bearing of its pos): the point of the
                     // observed line nearest to that pos seen from the predicted pose (observe_point)
@@ -1598,7 +1582,6 @@ template <int HYP, int MODE>
 __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     WAVE_CENSUS(a, a.fixup ? WC_FIXUP : WC_POST);
-    if ((a.cons_prio >> 4) & 3) set_prio_level((a.cons_prio >> 4) & 3);
     for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
 #ifdef LSLAM_STAMPS
         const uint64_t t0 = lslam_stamp();
@@ -1635,8 +1618,6 @@ __global__ __launch_bounds__(256) void ukf_group_kernel(const KArgs a, int Pg, i
     const int wave = (int)blockIdx.x * (int)(blockDim.x >> 6) + ((int)threadIdx.x >> 6);
     const int s = wave * (64 / Pg) + lane / Pg;
     WAVE_CENSUS(a, WC_UKF);
-    const int uprio = (a.cons_prio & 256) ? (a.cons_prio >> 6) & 3 : (a.cons_prio >> 4) & 3;  // default: the post's
-    if (uprio) set_prio_level(uprio);
     if (s >= B.n_scans) return;  // whole groups only: the butterfly stays inside a group
     double x[3], Pm[9];
     for (int i = 0; i < 3; i++) x[i] = B.ukf_x[3 * (size_t)s + i];
@@ -1675,10 +1656,10 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
     int Pg = 1;
     while (Pg < (n_landmarks + 1) / 2 && Pg < 64) Pg <<= 1;
     const int per = 64 / Pg;
-    // waves per workgroup (LSLAM_UKF_WG, 1..4): a workgroup's waves go to different SIMDs of one
-    // CU, so 4-wave groups keep the 253-VGPR waves at one per SIMD, where single-wave groups
-    // stack two on some SIMDs (full register file) and hold the next producer off that CU
-    static const int wpg = [] { const char *e = getenv("LSLAM_UKF_WG"); const int v = e ? atoi(e) : 4; return v >= 1 && v <= 4 ? v : 4; }();
+    // waves per workgroup: a workgroup's waves go to different SIMDs of one CU, so 4-wave groups
+    // keep the 253-VGPR waves at one per SIMD, where single-wave groups stack two on some SIMDs
+    // (full register file) and hold the next producer off that CU
+    constexpr int wpg = 4;
     const int nwaves = (k.b.n_scans + per - 1) / per;
     const dim3 grid((unsigned)((nwaves + wpg - 1) / wpg)), block(64 * wpg);
     const int var = (trace ? UKF_VAR_TRACE : 0) | (k.b.ukf_sigmas ? UKF_VAR_SIGMAS : 0);
@@ -1694,194 +1675,136 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
 // rng_kernel: the chained parity stream of one scan -> every chunk's draws
 // (lslam_rng_pipe.h)
 // ------------------------------------------------------------------------
-// PPW parser waves (one scan each) per workgroup.  Launched with 64 * PPW threads (the
-// default) each parser twists its own blocks; launched with 64 * (PPW + 1) (LSLAM_RNG_SELF=0)
-// the last wave is a helper that twists for all PPW parsers (asleep most of the time).  A
-// 4096-scan batch then holds 4 (or 5) waves per SIMD: the previous call's consumers run
-// beside it in the other slots.
-template <typename JT, int PPW>
-__global__ __launch_bounds__(64 * (PPW + 1)) void rng_kernel(const KArgs a) {
+// RNG_PPW parser waves (one scan each) per workgroup, each twisting its own MT blocks: a
+// 4096-scan batch holds 4 waves per SIMD, and the previous call's consumers run beside it in
+// the other wave slots.
+constexpr int RNG_PPW = 4;
+template <typename JT>
+__global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = (int)threadIdx.x & 63;
     const int wave = uni((int)threadIdx.x >> 6);
     const lslam_scan_batch &B = a.b;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : (uint32_t)a.T + 1u;  // draws of this launch
-    WAVE_CENSUS(a, wave < PPW ? WC_RNG_PARSER : WC_RNG_HELPER);
-    auto pipe_of = [&](int j) {
-        RngPipe rp;
-        unsigned char *base = smem + (size_t)j * a.rng_pipe_bytes;
+    WAVE_CENSUS(a, WC_RNG_PARSER);
+    RngPipe rp;
+    {
+        unsigned char *base = smem + (size_t)wave * a.rng_pipe_bytes;
         rp.blk = (uint32_t *)(base + a.off_blk);
         rp.fl = (lds_flag_t *)(base + a.off_fl);
-        rp.tbl = (uint32_t *)(base + a.off_tbl);
+        rp.tbl = nullptr;
         rp.tblK = 0;
-        rp.self_twist = blockDim.x == 64u * PPW;  // launched without the helper wave
-        return rp;
-    };
-    // Shared reject tables (off_stbl >= 0): the workgroup's parsers claim up to two table Ks
-    // (K = N-1 <= RT_KMAX of their chunks) and the workgroup loads those two tables once; a
-    // chunk whose K got no slot is parsed in mask mode (same steps).  Per-parser tables held
-    // 4 x 3.5 KiB of each workgroup's LDS: ~142 of a CU's 160 KiB with 4 workgroups, which
-    // left the consumers beside the producer ~4 consensus waves per CU (wave census).
-    int *kslot = a.off_stbl >= 0 ? (int *)(smem + a.off_stbl) : nullptr;
-    uint32_t *stbl = a.off_stbl >= 0 ? (uint32_t *)(smem + a.off_stbl + 16) : nullptr;
-    if (kslot && threadIdx.x < 2) kslot[threadIdx.x] = 0;
-    if (wave < PPW) {
-        const int s0 = (int)blockIdx.x * PPW + wave;
-        RngPipe rp = pipe_of(wave);
-        // block 0 = the initial state (raw); flags
-        if (s0 < B.n_scans) {
-            if (B.mt_state_in) {
-                const uint32_t *src = B.mt_state_in + (size_t)s0 * 625;
-                for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
-            } else {
-                mt_seed(rp.blk, B.seeds ? B.seeds[s0] : 0u, lane);
-            }
+    }
+    // Shared reject tables: the workgroup's parsers claim up to two table Ks (K = N-1 <= RT_KMAX
+    // of their chunks) and the workgroup loads those two tables once; a chunk whose K got no slot
+    // is parsed in mask mode (same steps).  Per-parser tables held 4 x 3.5 KiB of each
+    // workgroup's LDS: ~142 of a CU's 160 KiB with 4 workgroups, which left the consumers beside
+    // the producer ~4 consensus waves per CU (wave census).
+    int *kslot = (int *)(smem + a.off_stbl);
+    uint32_t *stbl = (uint32_t *)(smem + a.off_stbl + 16);
+    if (threadIdx.x < 2) kslot[threadIdx.x] = 0;
+    const int s = (int)blockIdx.x * RNG_PPW + wave;
+    // block 0 = the initial state (raw); flags
+    if (s < B.n_scans) {
+        if (B.mt_state_in) {
+            const uint32_t *src = B.mt_state_in + (size_t)s * 625;
+            for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
+        } else {
+            mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
         }
-        if (lane < F_NFLAGS) rp.fl[lane] = 0;
-        if (s0 >= B.n_scans && lane == 0) rp.fl[F_BLKUSE] = -1;  // no scan: nothing to twist
+    }
+    if (lane < F_NFLAGS) rp.fl[lane] = 0;
+    __syncthreads();
+    if (s < B.n_scans && lane == 0) {
+        for (int c = B.scan_chunk_off[s]; c < B.scan_chunk_off[s + 1]; c++) {
+            const int K = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c] - 1;
+            if (K < 2 || K > (int)RT_KMAX) continue;
+            const int o = atomicCAS(kslot, 0, K);
+            if (o == 0 || o == K) continue;
+            (void)atomicCAS(kslot + 1, 0, K);  // taken by another K: no table, mask mode
+        }
     }
     __syncthreads();
-    if (kslot) {
-        const int s0 = (int)blockIdx.x * PPW + wave;
-        if (wave < PPW && s0 < B.n_scans && lane == 0 && a.rt_all) {
-            for (int c = B.scan_chunk_off[s0]; c < B.scan_chunk_off[s0 + 1]; c++) {
-                const int K = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c] - 1;
-                if (K < 2 || K > (int)RT_KMAX) continue;
-                const int o = atomicCAS(kslot, 0, K);
-                if (o == 0 || o == K) continue;
-                (void)atomicCAS(kslot + 1, 0, K);  // taken by another K: no table, mask mode
-            }
-        }
-        __syncthreads();
-        for (int t = 0; t < 2; t++) {
-            const int K = kslot[t];
-            if (K == 0) continue;
-            const uint32_t mK = 0xffffffffu >> __clz(K);
-            const uint4 *src = (const uint4 *)(a.rt_all + (size_t)(K - 2) * RT_DWORDS);
-            uint4 *dst = (uint4 *)(stbl + t * RT_DWORDS);
-            const uint32_t n4 = (mK + 1u) * RT_ST / 4u;
-            for (uint32_t e = threadIdx.x; e < n4; e += blockDim.x) dst[e] = src[e];
-        }
-        __syncthreads();
+    for (int t = 0; t < 2; t++) {
+        const int K = kslot[t];
+        if (K == 0) continue;
+        const uint32_t mK = 0xffffffffu >> __clz(K);
+        const uint4 *src = (const uint4 *)(a.rt_all + (size_t)(K - 2) * RT_DWORDS);
+        uint4 *dst = (uint4 *)(stbl + t * RT_DWORDS);
+        const uint32_t n4 = (mK + 1u) * RT_ST / 4u;  // rows 0..mK (mK + 1 >= 4, a power of two)
+        for (uint32_t e = threadIdx.x; e < n4; e += blockDim.x) dst[e] = src[e];
     }
-    if (wave < PPW) {
-        const int s = (int)blockIdx.x * PPW + wave;
-        RngPipe rp = pipe_of(wave);
+    __syncthreads();
 #ifdef LSLAM_WSTAMPS
-        for (int k = 0; k < 8; k++) rp.wacc[k] = 0;
+    for (int k = 0; k < 8; k++) rp.wacc[k] = 0;
 #endif
 #ifdef LSLAM_STAMPS
-        for (int k = 0; k < 8; k++) rp.acc[k] = 0;
-        const uint64_t t_start = lslam_stamp();
-        const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 8; k++) rp.acc[k] = 0;
+    const uint64_t t_start = lslam_stamp();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (s >= B.n_scans) return;
-        // ---- parser: its chain is the kernel's critical path
-        const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
-        rp.total_steps = 0;
-        rp.done_steps = 0;
-        for (int c = c0; c < c1; c++) {
-            const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
-            if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
+    if (s >= B.n_scans) return;
+    // ---- parser: its chain is the kernel's critical path
+    const int c0 = B.scan_chunk_off[s], c1 = B.scan_chunk_off[s + 1];
+    rp.total_steps = 0;
+    rp.done_steps = 0;
+    for (int c = c0; c < c1; c++) {
+        const int N = B.chunk_pt_off[c + 1] - B.chunk_pt_off[c];
+        if (N >= 3) rp.total_steps += D * (uint32_t)(N - 1);
+    }
+    rp_set_schedule(rp);
+    rp.prio = RP_PRIO_TOP;
+    set_prio_level(RP_PRIO_TOP);
+    int blkno = 0;
+    int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
+    JT *J = (JT *)a.jbuf;
+    for (int c = c0; c < c1; c++) {
+        const int p0 = B.chunk_pt_off[c];
+        const int N = B.chunk_pt_off[c + 1] - p0;
+        if (N < 3) continue;
+        JT *Jc = J + (size_t)D * (size_t)p0;
+        const int K = N - 1;
+        const bool tbl = K <= (int)RT_KMAX && (kslot[0] == K || kslot[1] == K);
+        if (tbl) {
+            rp.tbl = stbl + (kslot[0] == K ? 0 : RT_DWORDS);
+            rp.tblK = (uint32_t)K;
         }
-        rp_set_schedule(rp);
-        rp.prio = RP_PRIO_TOP;
-        set_prio_level(RP_PRIO_TOP);
-        int blkno = 0;
-        int pos = B.mt_state_in ? uni((int)B.mt_state_in[(size_t)s * 625 + 624]) : MT_N;
-        JT *J = (JT *)a.jbuf;
-        for (int c = c0; c < c1; c++) {
-            const int p0 = B.chunk_pt_off[c];
-            const int N = B.chunk_pt_off[c + 1] - p0;
-            if (N < 3) continue;
-            JT *Jc = J + (size_t)D * (size_t)p0;
-            bool tbl = a.rt_all && (uint32_t)N - 1u <= RT_KMAX;
-            if (tbl && kslot) {  // the workgroup's shared tables
-                const int K = N - 1;
-                tbl = kslot[0] == K || kslot[1] == K;
-                if (tbl) {
-                    rp.tbl = stbl + (kslot[0] == K ? 0 : RT_DWORDS);
-                    rp.tblK = (uint32_t)K;
-                }
-            } else if (tbl && rp.tblK != (uint32_t)N - 1u) {
-                rt_load(rp, a.rt_all, (uint32_t)N - 1u, lane);
-            }
-            if (tbl && N - 1 >= 64) parse_chunk_tbl<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
-            else if (tbl) parse_chunk_tbl<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
-            else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
-            else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
-        }
-        lds_flag_put(rp.fl + F_BLKUSE, -1);  // this pipe needs no more blocks
-        wake_helper();
-        if (pos > MT_N) {  // the last window ran across the block end: its block is in (numpy twisted too)
-            blkno += 1;
-            pos -= MT_N;
-        }
-        if (B.mt_state_out) {
-            uint32_t *o = B.mt_state_out + (size_t)s * 625;
-            const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
-            for (int i = lane; i < MT_N; i += 64) o[i] = kb[i];
-            if (lane == 0) o[624] = (uint32_t)pos;
-        }
+        if (tbl && K >= 64) parse_chunk_tbl<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+        else if (tbl) parse_chunk_tbl<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+        else if (N >= 65) parse_chunk<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+        else parse_chunk<false>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);
+    }
+    if (pos > MT_N) {  // the last window ran across the block end: its block is in (numpy twisted too)
+        blkno += 1;
+        pos -= MT_N;
+    }
+    if (B.mt_state_out) {
+        uint32_t *o = B.mt_state_out + (size_t)s * 625;
+        const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
+        for (int i = lane; i < MT_N; i += 64) o[i] = kb[i];
+        if (lane == 0) o[624] = (uint32_t)pos;
+    }
 #ifdef LSLAM_STAMPS
-        rp.acc[7] = lslam_stamp() - t_start;
-        rp.acc[4] = rt_start;  // residency census (100 MHz chip-wide clock)
-        rp.acc[3] = __builtin_amdgcn_s_memrealtime();
+    rp.acc[7] = lslam_stamp() - t_start;
+    rp.acc[4] = rt_start;  // residency census (100 MHz chip-wide clock)
+    rp.acc[3] = __builtin_amdgcn_s_memrealtime();
 #ifdef LSLAM_WSTAMPS
-        if (a.dbg && lane == 0) {
-            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
-            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + 8 + k] = rp.wacc[k];
-        }
-        if (false) {
+    if (a.dbg && lane == 0) {
+        for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
+        for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + 8 + k] = rp.wacc[k];
+    }
 #else
-        if (a.dbg && lane == 0) {
-#endif
-            for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
-            // placement census: HW_ID simd / cu / se of the parser, xcc
-            a.dbg[(size_t)s * 16 + 8] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
-            a.dbg[(size_t)s * 16 + 9] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (8 << 6) | (3 << 11));
-            a.dbg[(size_t)s * 16 + 10] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (13 << 6) | (2 << 11));
-            a.dbg[(size_t)s * 16 + 11] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
-            a.dbg[(size_t)s * 16 + 13] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (12 << 6) | (0 << 11));
-        }
-#endif
-    } else {
-        // ---- helper: twists on demand for every parser of the workgroup, asleep otherwise
-        // (block 0 and the flags are in: the workgroup barriers above)
-        __builtin_amdgcn_s_setprio(3);
-#ifdef LSLAM_STAMPS
-        if (a.dbg && lane == 0)
-            for (int j = 0; j < PPW; j++)
-                if ((int)blockIdx.x * PPW + j < B.n_scans)
-                    a.dbg[((size_t)blockIdx.x * PPW + j) * 16 + 12] =
-                        (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
-#endif
-        int produced[PPW];
-#pragma unroll
-        for (int j = 0; j < PPW; j++) produced[j] = 0;
-        for (;;) {
-            bool busy = false, live = false;
-#pragma unroll
-            for (int j = 0; j < PPW; j++) {
-                RngPipe rp = pipe_of(j);
-                const int use = lds_flag_get(rp.fl + F_BLKUSE);
-                if (use < 0) continue;  // parser finished
-                live = true;
-                if (use == produced[j]) {
-                    mt_twist_oop(rp.blk + (produced[j] & 1) * MT_N, rp.blk + ((produced[j] + 1) & 1) * MT_N, lane);
-                    if (((produced[j] + 1) & 1) == 0) {  // pad after slot 1 = the new block's head
-                        rp.blk[2 * MT_N + lane] = rp.blk[lane];
-                        wave_lds_sync();
-                    }
-                    produced[j] += 1;
-                    lds_flag_put(rp.fl + F_BLK, produced[j]);
-                    busy = true;
-                }
-            }
-            if (!live) break;
-            if (!busy) __builtin_amdgcn_s_sleep(127);  // until a parser's s_wakeup
-        }
+    if (a.dbg && lane == 0) {
+        for (int k = 0; k < 8; k++) a.dbg[(size_t)s * 16 + k] = rp.acc[k];
+        // placement census: HW_ID simd / cu / se of the parser, xcc
+        a.dbg[(size_t)s * 16 + 8] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));
+        a.dbg[(size_t)s * 16 + 9] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (8 << 6) | (3 << 11));
+        a.dbg[(size_t)s * 16 + 10] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (13 << 6) | (2 << 11));
+        a.dbg[(size_t)s * 16 + 11] = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+        a.dbg[(size_t)s * 16 + 13] = (uint32_t)__builtin_amdgcn_s_getreg(4 | (12 << 6) | (0 << 11));
     }
+#endif
+#endif
 }
 
 // ------------------------------------------------------------------------
@@ -1895,7 +1818,6 @@ __global__ __launch_bounds__(64) void resolve_kernel(const KArgs a) {
     const lslam_scan_batch &B = a.b;
     const uint32_t Dall = (uint32_t)a.T + 1u;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
@@ -1920,7 +1842,6 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
     const lslam_scan_batch &B = a.b;
     const uint32_t Dall = (uint32_t)a.T + 1u;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     for (int c = blockIdx.x; c < B.n_chunks; c += gridDim.x) {
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
@@ -1972,10 +1893,6 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
 // i at byte K - i); the lowest group may start up to 15 bytes before the row (the
 // previous row, or the slot's front pad JBUF_FRONT) and walks only i <= K.
 constexpr int RR_GROUPS = 8;  // K <= 127
-#ifndef LSLAM_RR_FAST
-#define LSLAM_RR_FAST 1
-#endif
-constexpr bool RR_FAST = LSLAM_RR_FAST != 0;  // 5-VALU steps for i <= 64 (rr_step_nx)
 constexpr size_t JBUF_FRONT = 64;  // bytes of a producer slot before its steps
 // One step of both trackers, c = (j == c) ? i : c.  The two trackers are independent
 // chains, so both compares are issued (masks in two SGPR pairs) before both selects; the
@@ -2055,7 +1972,7 @@ __device__ __forceinline__ void rr_walk_fast(const uint32_t (&w)[4], uint32_t K,
 
 template <bool CHECK, uint32_t T>
 __device__ __forceinline__ void rr_walk_group(const uint32_t (&ws)[4], uint32_t K, uint32_t &c0, uint32_t &c1) {
-    if constexpr (T <= 3u && RR_FAST) {
+    if constexpr (T <= 3u) {  // 5-VALU steps for i <= 64 (rr_step_nx)
         constexpr uint32_t i0 = 16u * T + 1u;
         const uint32_t j0 = __builtin_amdgcn_ubfe(ws[3], 24u, 32u - (uint32_t)__builtin_clz(i0));  // byte 15
         rr_walk_fast<CHECK, T, 0>(ws, K, c0, c1, j0);
@@ -2082,112 +1999,6 @@ __device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_
     rr_walk_groups<0>(w, K, K >> 4, c0, c1);  // K >> 4 groups with all 16 steps <= K
 }
 
-// Two groups of 64 draws per wave (lane l walks draws d and d + 64 of its chunk at once):
-// the two walks are independent chains, interleaved step by step (four compares, then four
-// selects), so a wave keeps twice the work in flight.  Beside the producer a SIMD holds ~3
-// consumer waves and the walk is a dependent compare -> select chain per step: C3's 101 draws
-// per chunk were two waves of which the second had 37 live lanes.
-template <uint32_t I>
-__device__ __forceinline__ void rr_step2(uint32_t ja, uint32_t jb, uint32_t &a0, uint32_t &a1, uint32_t &b0,
-                                         uint32_t &b1) {
-    uint64_t m0, m1, m2, m3;
-    uint32_t iv;
-    asm volatile(
-        "v_cmp_eq_u32_e64 %[m0], %[ja], %[a0]\n\t"
-        "v_cmp_eq_u32_e64 %[m1], %[ja], %[a1]\n\t"
-        "v_cmp_eq_u32_e64 %[m2], %[jb], %[b0]\n\t"
-        "v_cmp_eq_u32_e64 %[m3], %[jb], %[b1]\n\t"
-        "v_mov_b32 %[iv], %[i]\n\t"
-        "v_cndmask_b32_e64 %[a0], %[a0], %[iv], %[m0]\n\t"
-        "v_cndmask_b32_e64 %[a1], %[a1], %[iv], %[m1]\n\t"
-        "v_cndmask_b32_e64 %[b0], %[b0], %[iv], %[m2]\n\t"
-        "v_cndmask_b32_e64 %[b1], %[b1], %[iv], %[m3]"
-        : [a0] "+v"(a0), [a1] "+v"(a1), [b0] "+v"(b0), [b1] "+v"(b1), [m0] "=&s"(m0), [m1] "=&s"(m1),
-          [m2] "=&s"(m2), [m3] "=&s"(m3), [iv] "=&v"(iv)
-        : [ja] "v"(ja), [jb] "v"(jb), [i] "i"(I));
-}
-
-template <bool CHECK, uint32_t T, int U>
-__device__ __forceinline__ void rr_walk_from2(const uint32_t (&wa)[4], const uint32_t (&wb)[4], uint32_t K,
-                                              uint32_t &a0, uint32_t &a1, uint32_t &b0, uint32_t &b1) {
-    if constexpr (U < 16) {
-        constexpr uint32_t i = 16u * T + 1u + (uint32_t)U;
-        if constexpr (i >= 2u) {
-            if (CHECK && i > K) return;
-            constexpr int off = 15 - U;
-            constexpr uint32_t nb = 32u - (uint32_t)__builtin_clz(i);
-            const uint32_t ja = __builtin_amdgcn_ubfe(wa[off >> 2], (uint32_t)(8 * (off & 3)), nb);
-            const uint32_t jb = __builtin_amdgcn_ubfe(wb[off >> 2], (uint32_t)(8 * (off & 3)), nb);
-            rr_step2<i>(ja, jb, a0, a1, b0, b1);
-        }
-        rr_walk_from2<CHECK, T, U + 1>(wa, wb, K, a0, a1, b0, b1);
-    }
-}
-
-template <uint32_t T>
-__device__ __forceinline__ void rr_walk_groups2(const uint4 (&wa)[RR_GROUPS], const uint4 (&wb)[RR_GROUPS], uint32_t K,
-                                                uint32_t nfull, uint32_t &a0, uint32_t &a1, uint32_t &b0,
-                                                uint32_t &b1) {
-    if constexpr (T < (uint32_t)RR_GROUPS) {
-        const uint32_t xa[4] = {wa[T].x, wa[T].y, wa[T].z, wa[T].w};
-        const uint32_t xb[4] = {wb[T].x, wb[T].y, wb[T].z, wb[T].w};
-        if (T < nfull) {
-            rr_walk_from2<false, T, 0>(xa, xb, K, a0, a1, b0, b1);
-            rr_walk_groups2<T + 1>(wa, wb, K, nfull, a0, a1, b0, b1);
-        } else if (T == nfull) {
-            rr_walk_from2<true, T, 0>(xa, xb, K, a0, a1, b0, b1);
-        }
-    }
-}
-
-__device__ __forceinline__ void rr_store(const KArgs &a, int c, uint32_t d, uint32_t j1w, uint32_t c0, uint32_t c1) {
-    const uint32_t Dall = (uint32_t)a.T + 1u;
-    const uint32_t j1 = (j1w >> 24) & 1u;  // byte K - 1: step 1
-    int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)(a.ep_d0 + d);
-    draws[0] = (int32_t)((j1 == 0u) ? c1 : c0);
-    draws[1] = (int32_t)((j1 == 0u) ? c0 : c1);
-}
-
-__global__ __launch_bounds__(64) void resolve_reg8x2_kernel(const KArgs a) {
-    const int lane = (int)threadIdx.x;
-    const lslam_scan_batch &B = a.b;
-    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : (uint32_t)a.T + 1u;
-    const int np = (int)((D + 127u) >> 7);  // waves per chunk: lanes x 2 = 128 draws
-    WAVE_CENSUS(a, WC_RESOLVE);
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
-    const int64_t total = (int64_t)B.n_chunks * np;
-    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
-        const int c = (int)(e / np);
-        const uint32_t d0 = 128u * (uint32_t)(e - (int64_t)c * np);
-        const int p0 = B.chunk_pt_off[c];
-        const int N = B.chunk_pt_off[c + 1] - p0;
-        if (N < 3) continue;
-        const uint32_t K = (uint32_t)N - 1u;  // <= 127 (host)
-        const uint8_t *J = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0;
-        const uint32_t da = d0 + (uint32_t)lane, db = da + 64u;
-        const uint8_t *ra = J + (size_t)(da < D ? da : 0u) * K;
-        uint4 wa[RR_GROUPS];
-#pragma unroll
-        for (int t = 0; t < RR_GROUPS; t++)
-            if ((uint32_t)(16 * t) < K) wa[t] = load16_unaligned(ra + (int)K - 16 * (t + 1));
-        if (d0 + 64u < D) {  // wave-uniform: the second group has live draws
-            const uint8_t *rb = J + (size_t)(db < D ? db : 0u) * K;
-            uint4 wb[RR_GROUPS];
-#pragma unroll
-            for (int t = 0; t < RR_GROUPS; t++)
-                if ((uint32_t)(16 * t) < K) wb[t] = load16_unaligned(rb + (int)K - 16 * (t + 1));
-            uint32_t a0 = 0, a1 = 1, b0 = 0, b1 = 1;
-            rr_walk_groups2<0>(wa, wb, K, K >> 4, a0, a1, b0, b1);
-            if (da < D) rr_store(a, c, da, wa[0].w, a0, a1);
-            if (db < D) rr_store(a, c, db, wb[0].w, b0, b1);
-        } else {
-            uint32_t a0 = 0, a1 = 1;
-            rr_walk_row(wa, K, a0, a1);
-            if (da < D) rr_store(a, c, da, wa[0].w, a0, a1);
-        }
-    }
-}
-
 __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
@@ -2195,7 +2006,6 @@ __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
     const int ng = (int)((D + 63u) >> 6);  // waves per chunk: lanes = 64 draws
     WAVE_CENSUS(a, WC_RESOLVE);
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     const int64_t total = (int64_t)B.n_chunks * ng;
     for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
         const int c = (int)(e / ng);
@@ -2220,81 +2030,8 @@ __global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
     }
 }
 
-// Chunks whose steps do not fit the 16 KiB stage (C5: 2049 draws x 4095 steps
-// x 2 B = 16.8 MB per chunk).  One wave per (chunk, group of 64 draws), lanes =
-// draws as in resolve_draws_fwd, but the steps stream through an LDS tile of
-// [64 draws][RB steps] filled with row-contiguous (coalesced) loads: a lane
-// walking its own draw straight from HBM touches 64 cache lines per load and
-// left C5's resolve at 150 ms per call.  Rows are padded to an odd number of
-// dwords, so the lanes' reads of one step column hit distinct banks.
-constexpr int RB = 128;                 // steps per tile (= 2 columns per lane in the fill)
-constexpr int RB_STRIDE = RB + 2;       // row stride in elements (u16: 65 dwords; u8: pad to 33 dwords below)
-template <typename JT>
-__global__ __launch_bounds__(64) void resolve_big_kernel(const KArgs a, int ngroups) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int STRIDE = sizeof(JT) == 2 ? RB_STRIDE : RB + 4;
-    JT *tile = (JT *)smem;
-    const int lane = (int)threadIdx.x;
-    const lslam_scan_batch &B = a.b;
-    const uint32_t Dall = (uint32_t)a.T + 1u;
-    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
-    const int64_t total = (int64_t)B.n_chunks * ngroups;
-    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
-        const int c = (int)(e / ngroups), g = (int)(e - (int64_t)c * ngroups);
-        const int p0 = B.chunk_pt_off[c];
-        const int N = B.chunk_pt_off[c + 1] - p0;
-        if (N < 3) continue;
-        const uint32_t K = (uint32_t)N - 1u;
-        const uint32_t d0 = (uint32_t)g * 64u;
-        const uint32_t nd = min(64u, D - d0);
-        const JT *Jc = (const JT *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)d0 * K;  // row r = draw d0 + r
-        uint32_t c0 = 0, c1 = 1;
-        // forward scan i = 2..K reads memory offset K - i: tiles of i in [i0, i0 + RB)
-        for (uint32_t i0 = 2; i0 <= K; i0 += RB) {
-            const uint32_t i1 = min(i0 + (uint32_t)RB, K + 1u);  // exclusive
-            const uint32_t mlo = K - (i1 - 1u);                  // lowest memory offset of the tile
-            const uint32_t ncol = i1 - i0;
-            // 8 rows x 2 columns per lane in flight, then into LDS
-            for (uint32_t r0 = 0; r0 < nd; r0 += 8) {
-                JT v[8][2];
-#pragma unroll
-                for (int rr = 0; rr < 8; rr++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint32_t r = r0 + (uint32_t)rr, x = (uint32_t)lane + 64u * (uint32_t)h;
-                        v[rr][h] = (r < nd && x < ncol) ? Jc[(size_t)r * K + mlo + x] : (JT)0;
-                    }
-#pragma unroll
-                for (int rr = 0; rr < 8; rr++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint32_t r = r0 + (uint32_t)rr, x = (uint32_t)lane + 64u * (uint32_t)h;
-                        if (r < nd && x < ncol) tile[r * STRIDE + x] = v[rr][h];
-                    }
-            }
-            __syncthreads();
-            if ((uint32_t)lane < nd) {
-                const JT *trow = tile + lane * STRIDE;
-                for (uint32_t i = i0; i < i1; i++) {
-                    const uint32_t j = trow[K - i - mlo] & step_mask(i);
-                    c0 = (j == c0) ? i : c0;
-                    c1 = (j == c1) ? i : c1;
-                }
-            }
-            __syncthreads();
-        }
-        if ((uint32_t)lane < nd) {
-            const uint32_t d = d0 + (uint32_t)lane;
-            const uint32_t j1 = Jc[(size_t)lane * K + (K - 1u)] & 1u;
-            int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)a.ep_d0;
-            draws[2 * d] = (int32_t)((j1 == 0u) ? c1 : c0);
-            draws[2 * d + 1] = (int32_t)((j1 == 0u) ? c0 : c1);
-        }
-    }
-}
-
-// The same without LDS: one wave per (chunk, draw), lanes = 64 consecutive
+// Chunks whose steps do not fit the 16 KiB stage (C5: 2049 draws x 4095 steps x 2 B = 16.8 MB
+// per chunk), without LDS: one wave per (chunk, draw), lanes = 64 consecutive
 // steps i of the draw, so each load is one coalesced 128-byte (u16) read
 // straight from HBM and a wave keeps RW windows of loads in flight.  The
 // trackers c0, c1 are wave-uniform: a window's matches j_i == c come out of one
@@ -2307,7 +2044,6 @@ __global__ __launch_bounds__(64) void resolve_walk_kernel(const KArgs a) {
     const lslam_scan_batch &B = a.b;
     const uint32_t Dall = (uint32_t)a.T + 1u;
     const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws of this launch (from ep_d0)
-    if (a.cons_prio & 3) set_prio_level(a.cons_prio & 3);
     const int64_t total = (int64_t)B.n_chunks * D;
     for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
         const int c = (int)(e / D);
@@ -2454,17 +2190,9 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
 }
 
 template <int HYP>
-#ifndef LSLAM_CHUNK_WAVES
-#define LSLAM_CHUNK_WAVES 0  // minimum waves per SIMD the allocation must allow (0: the compiler chooses; A/B)
-#endif
-#if LSLAM_CHUNK_WAVES > 0
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSLAM_CHUNK_WAVES))) void chunk_kernel(const KArgs a) {
-#else
 __global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
-#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     WAVE_CENSUS(a, WC_CHUNK);
-    if ((a.cons_prio >> 2) & 3) set_prio_level((a.cons_prio >> 2) & 3);
     for (int c = blockIdx.x; c < a.b.n_chunks; c += gridDim.x) {
         chunk_body<HYP>(a, c, smem);
         __syncthreads();
@@ -2913,6 +2641,7 @@ __global__ __launch_bounds__(256) void polar_kernel(const double *__restrict__ t
 constexpr int LSLAM_EV_RING = 64;
 constexpr int LSLAM_MAX_OUTS = 48;
 
+constexpr int NSLOTS = 2;  // producer slots in the ring
 struct lslam_ctx {
     int device;
     hipStream_t stream;
@@ -2933,36 +2662,23 @@ struct lslam_ctx {
     void *cscr;
     size_t cscr_bytes;
     // grid cap of the one-wave consumer kernels (resolve, chunk, fix-up, post)
-    int consumer_wgs;
-    int resolve_walk;  // unstaged resolves: lanes = steps (env LSLAM_RESOLVE_TILED=1: LDS tiles)
-    int epoch_serial;  // env LSLAM_EPOCH_SERIAL=1: epochs one after the other on the ctx stream
-    int ukf_lanes;     // fused UKF on lane groups (env LSLAM_UKF_LANES=0: one wave per scan)
-    int ukf_side_mt;   // env LSLAM_UKF_SIDE=1: an independent UKF on the side stream in parity mode too (A/B)
-    int resolve_reg;   // staged-size u8 resolves from registers (env LSLAM_RESOLVE_REG=0: LDS stage, 2: resolve_reg_kernel)
     int resolve_beside;  // this call's resolves will likely run beside the next call's producer
     int n_cus;         // compute units of the device
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
-    // parser waves per producer workgroup (one helper each)
-    int rng_ppw;
-    // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h); null = off
+    // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h)
     uint32_t *rt_all;
     size_t steps_budget;  // producer slot budget (prepare_steps)
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
     // end-of-scan MT state), each released by an event once its consumers ran.
+    // (Measured and dropped at r04: a third slot, 0.79-0.86 vs 0.76 ms per C3 step; the resolve
+    // on a stream of its own after its producer, 0.871 vs 0.763 ms.)
     hipStream_t pstream;
-    int nslots;                  // producer slots in the ring (LSLAM_SLOTS, 2 or 3)
-    void *pslot[3];
+    void *pslot[NSLOTS];
     size_t pslot_bytes;
     int next_slot;
-    hipEvent_t ev_slot_free[3];  // on stream, after the slot's resolve + fix-up
+    hipEvent_t ev_slot_free[NSLOTS];  // on stream, after the slot's resolve + fix-up
     hipEvent_t ev_produced;      // on pstream, after rng_kernel
-    // The resolve of a one-launch producer runs on its own stream after the producer, off the
-    // ctx chain (LSLAM_RESOLVE_STREAM): its draws go to the slot, and the ctx stream waits for
-    // ev_resolved before the consensus.
-    int resolve_stream;
-    hipStream_t rstream;
-    hipEvent_t ev_resolved;      // on rstream, after the resolve
     hipEvent_t ev_copy;          // on stream, after the latest lslam_h2d / lslam_memset
     // destinations written by copies since the producer last waited for ev_copy: the producer
     // waits only if one of them is its input (seeds, CSR, MT state), so an xy upload per call
@@ -2989,9 +2705,9 @@ struct lslam_ctx {
     // speculative producer (map mode): a call whose only producer hazard is the previous call's
     // mt_state_out parses from the previous producer's end state (its slot's state area) without
     // waiting for that call's fix-up; the fix-up replays the scans it replayed (spec_dirty)
-    int speculate;            // env LSLAM_MT_SPECULATE=0: wait for the fix-up (A/B)
+    int speculate;            // env LSLAM_MT_SPECULATE=0: wait for the fix-up (test_gpu_speculate.py)
     int spec_ok;              // the previous call was a one-epoch pipeline call with dirty flags
-    int spec_run;             // consecutive speculative calls (bounded by LSLAM_SPEC_RESYNC)
+    int spec_run;             // consecutive speculative calls (bounded by SPEC_RESYNC)
     const uint32_t *prev_state_scr;
     int prev_spec_scans;
     uint8_t *spec_dirty[2];   // [n_scans] replayed-by-fix-up flags, by call parity
@@ -3001,11 +2717,7 @@ struct lslam_ctx {
 
 static thread_local std::string g_err;
 
-static size_t default_steps_budget() {
-    const char *e = getenv("LSLAM_STEPS_BUDGET");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? (size_t)v : ((size_t)2 << 30);
-}
+static size_t default_steps_budget() { return (size_t)2 << 30; }  // lslam_set_steps_budget
 
 // rows v = 0..127 of every K = 2..127, built once per process (rt_word, lslam_rng_pipe.h)
 static const std::vector<uint32_t> &reject_tables() {
@@ -3088,46 +2800,13 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->escr_bytes = 0;
     c->cscr = nullptr;
     c->cscr_bytes = 0;
-    c->consumer_wgs = 1 << 30;
-    {
-        const char *e = getenv("LSLAM_RESOLVE_TILED");
-        c->resolve_walk = (e && atoi(e) != 0) ? 0 : 1;
-    }
-    {
-        const char *e = getenv("LSLAM_EPOCH_SERIAL");
-        c->epoch_serial = (e && atoi(e) != 0) ? 1 : 0;
-    }
-    {
-        const char *e = getenv("LSLAM_UKF_LANES");
-        c->ukf_lanes = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    {
-        const char *e = getenv("LSLAM_UKF_SIDE");
-        c->ukf_side_mt = (e && atoi(e) != 0) ? 1 : 0;
-    }
-    {
-        const char *e = getenv("LSLAM_RESOLVE_REG");
-        // 2: the 16-step walk, 3: two groups of 64 draws per wave (A/B)
-        c->resolve_reg = e ? (atoi(e) == 3 ? 3 : atoi(e) == 2 ? 2 : atoi(e) == 0 ? 0 : 1) : 1;
-    }
     c->resolve_beside = 0;
     c->timing_mask = 0xffffffffu;
-    c->rng_ppw = 4;
-    if (const char *e = getenv("LSLAM_RNG_PPW")) c->rng_ppw = atoi(e) == 1 ? 1 : 4;
     c->rt_all = nullptr;
     c->steps_budget = default_steps_budget();
-    if (const char *e = getenv("LSLAM_CONSUMER_WGS")) {
-        const int v = atoi(e);
-        if (v > 0) c->consumer_wgs = v;
-    }
     c->pstream = nullptr;
     c->ustream = nullptr;
-    c->rstream = nullptr;
-    c->pslot[0] = c->pslot[1] = c->pslot[2] = nullptr;
-    c->nslots = 2;
-    if (const char *e = getenv("LSLAM_SLOTS")) c->nslots = atoi(e) >= 3 ? 3 : 2;
-    c->resolve_stream = 0;
-    if (const char *e = getenv("LSLAM_RESOLVE_STREAM")) c->resolve_stream = atoi(e) != 0;
+    for (int i = 0; i < NSLOTS; i++) c->pslot[i] = nullptr;
     c->pslot_bytes = 0;
     c->next_slot = 0;
     c->speculate = 1;
@@ -3165,24 +2844,19 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
         if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
         HIPCHK(hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, hi_pri));
     }
-    for (int i = 0; i < 3; i++) HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[i], hipEventDisableTiming));
+    for (int i = 0; i < NSLOTS; i++) HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[i], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
-    HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_resolved, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->ev_ukf, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
-    for (int i = 0; i < 3; i++) HIPCHK(hipEventRecord(c->ev_slot_free[i], c->stream));
+    for (int i = 0; i < NSLOTS; i++) HIPCHK(hipEventRecord(c->ev_slot_free[i], c->stream));
     HIPCHK(hipEventRecord(c->ev_copy, c->stream));
     HIPCHK(hipEventRecord(c->ev_call, c->stream));
     {
-        const char *e = getenv("LSLAM_RNG_TABLE");  // 0: mask evaluation only (A/B)
-        if (!e || atoi(e) != 0) {
-            const std::vector<uint32_t> &t = reject_tables();
-            HIPCHK(hipMalloc(&c->rt_all, t.size() * 4));
-            HIPCHK(hipMemcpy(c->rt_all, t.data(), t.size() * 4, hipMemcpyHostToDevice));
-        }
+        const std::vector<uint32_t> &t = reject_tables();
+        HIPCHK(hipMalloc(&c->rt_all, t.size() * 4));
+        HIPCHK(hipMemcpy(c->rt_all, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     }
     *out = c;
     return LSLAM_OK;
@@ -3199,22 +2873,19 @@ int lslam_ctx_destroy(lslam_ctx *c) {
         }
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);
-    if (c->rstream) (void)hipStreamSynchronize(c->rstream);
     if (c->scr) (void)hipFree(c->scr);
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
-    for (int i = 0; i < 3; i++)
+    for (int i = 0; i < NSLOTS; i++)
         if (c->pslot[i]) (void)hipFree(c->pslot[i]);
     if (c->rt_all) (void)hipFree(c->rt_all);
     for (int i = 0; i < 2; i++)
         if (c->spec_dirty[i]) (void)hipFree(c->spec_dirty[i]);
-    hipEvent_t evs[8] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_slot_free[2], c->ev_produced,
-                         c->ev_copy,         c->ev_call,         c->ev_ukf,          c->ev_resolved};
+    hipEvent_t evs[6] = {c->ev_slot_free[0], c->ev_slot_free[1], c->ev_produced, c->ev_copy, c->ev_call, c->ev_ukf};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
     if (c->pstream) (void)hipStreamDestroy(c->pstream);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
-    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -3225,7 +2896,6 @@ int lslam_sync(lslam_ctx *c) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->pstream));
     HIPCHK(hipStreamSynchronize(c->ustream));
-    HIPCHK(hipStreamSynchronize(c->rstream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return LSLAM_OK;
 }
@@ -3520,20 +3190,6 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
     k.wcen_cap = g_wcen_cap;
     k.call_seq = g_call_seq;
 #endif
-    static const int cons_prio = [] {
-        // LSLAM_CONS_PRIO="[U]PCR": UKF (default: = post), post, chunk, resolve wave priorities
-        // (digits 0-3); default "000": every consumer at the lowest level, beside the parsers'
-        // levels 3..1 (measured: all consumers at 3 ran +40 %)
-        const char *e = getenv("LSLAM_CONS_PRIO");
-        if (!e || (strlen(e) != 3 && strlen(e) != 4)) e = "000";
-        if (strlen(e) == 4) {
-            const int u = (e[0] - '0') & 3;
-            e += 1;
-            return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4) | (u << 6) | 256;
-        }
-        return ((e[2] - '0') & 3) | (((e[1] - '0') & 3) << 2) | (((e[0] - '0') & 3) << 4);
-    }();
-    k.cons_prio = cons_prio;
     k.b = *b;
     if (p) {
         if (p->min_samples != 2) return set_err(LSLAM_ERR_UNSUPPORTED, "only min_samples == 2 (ransac_functions.py:11)");
@@ -3597,15 +3253,14 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         off = max(off, align16(8 * UkfLds::doubles(u->n_landmarks)));
     }
     k.hist_cap = b->max_scan_chunks > 0 ? b->max_scan_chunks : 1;
-    k.off_hist = off; off += align16(4 * k.hist_cap);
+    k.off_snap = off; off += (mode & MODE_RANSAC) ? align16(4 * MT_N) : 0;
     k.corg_cap = k.hist_cap;
     k.off_corg = off; off += align16(16 * k.corg_cap);
     k.off_zobs = off; off += (u && (u->flags & LSLAM_UKF_MAP)) ? align16(16 * k.corg_cap) : 0;
     k.lmk_cap = (mode & MODE_ASSOC) ? b->lmk_capacity : 0;
     if ((mode & MODE_ASSOC) && k.lmk_cap <= 0) return set_err(LSLAM_ERR_ARG, "lmk_capacity must be > 0");
     // the association-only post pass keeps a list of at most 64 entries in registers
-    static const bool lmk_reg_on = [] { const char *e = getenv("LSLAM_LMK_REG"); return !(e && atoi(e) == 0); }();
-    k.lmk_reg = (lmk_reg_on && mode == MODE_ASSOC && k.lmk_cap > 0 && k.lmk_cap <= 64 && k.off_recs >= 0 &&
+    k.lmk_reg = (mode == MODE_ASSOC && k.lmk_cap > 0 && k.lmk_cap <= 64 && k.off_recs >= 0 &&
                  !(u && (u->flags & LSLAM_UKF_MAP)) && b->landmarks) ? 1 : 0;
     k.off_lmk = off; off += k.lmk_reg ? 0 : align16((int)sizeof(lslam_landmark) * (k.lmk_cap > 0 ? k.lmk_cap : 1));
     k.off_vis = off; off += k.lmk_reg ? 0 : align16(8 * ((k.lmk_cap + 63) / 64 + 1));
@@ -3667,7 +3322,7 @@ static int run_scan_kernel(lslam_ctx *c, const KArgs &k, int lds, int timer) {
     });
     int st = timer_begin(c, timer);
     if (st) return st;
-    if (MODE == MODE_UKF && c->ukf_lanes && !(k.ukf.flags & LSLAM_UKF_MAP)) {  // stand-alone UKF: lane groups
+    if (MODE == MODE_UKF && !(k.ukf.flags & LSLAM_UKF_MAP)) {  // stand-alone UKF: lane groups
         launch_ukf_group(k, k.ukf.L, c->stream, false);
         HIPCHK(hipGetLastError());
     } else if (MODE == MODE_ASSOC || MODE == MODE_UKF) {  // stand-alone association / UKF: no producer beside them
@@ -3705,28 +3360,26 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
 }
 
 // rng_kernel LDS: two raw MT blocks + flags
-static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds, int ppw) {
+static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int N = b->max_chunk_points > 3 ? b->max_chunk_points : 3;
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
     int off = 0;
     k.off_blk = off; off += align16(4 * (2 * 624 + 64));  // two block slots + the head pad
     k.off_fl = off; off += align16(4 * F_NFLAGS);
-    // the reject table: table mode is chosen per chunk (N - 1 <= RT_KMAX), so a batch whose
-    // largest chunk is bigger may still parse its small chunks with it
-    static const bool shared = [] { const char *e = getenv("LSLAM_RT_SHARED"); return !(e && atoi(e) == 0); }();
-    k.off_stbl = -1;
-    k.off_tbl = off; off += (k.rt_all && !shared) ? align16(4 * RT_DWORDS) : 0;
     k.rng_pipe_bytes = off;
-    lds = off * ppw;
-    if (k.rt_all && shared) {  // two K claims (16 B) + two tables, after the pipes
-        k.off_stbl = lds;
-        lds += 16 + 2 * 4 * RT_DWORDS;
-    }
+    lds = off * RNG_PPW;
+    // two K claims (16 B) + two reject tables shared by the workgroup's parsers, after the
+    // pipes: table mode is chosen per chunk (N - 1 <= RT_KMAX), so a batch whose largest chunk
+    // is bigger may still parse its small chunks with them
+    k.off_stbl = lds;
+    lds += 16 + 2 * 4 * RT_DWORDS;
     return LSLAM_OK;
 }
 
+// consumer grids: one workgroup per item, at most 2^30 (kernels loop over their items)
 static inline unsigned launch_cap(const lslam_ctx *c, int64_t n) {
-    return (unsigned)(n < c->consumer_wgs ? (n > 0 ? n : 1) : c->consumer_wgs);
+    (void)c;
+    return (unsigned)(n < (1 << 30) ? (n > 0 ? n : 1) : (1 << 30));
 }
 
 static int ensure_scratch(lslam_ctx *c, size_t bytes) {
@@ -3759,7 +3412,7 @@ static void set_max_lds(F *fn) {
 // MT state.  The resolved draws live in the main-stream scratch unless the
 // caller asked for draws_out.
 // Epochs: when every scan is one chunk (C5) and the steps of all T + 1 draws
-// exceed the slot budget (LSLAM_STEPS_BUDGET bytes, default 2 GiB), the producer
+// exceed the slot budget (lslam_set_steps_budget, default 2 GiB), the producer
 // runs in launches of ep_nd draws, each resolved before its slot is reused; the
 // MT state chains through the slots' state areas.  k.ep_count launches.
 static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
@@ -3778,25 +3431,20 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     k.ep_count = (D + De - 1) / De;
     const size_t jbytes = ((size_t)De * per_draw + JBUF_FRONT + 64 + 255) & ~(size_t)255;
     const size_t sbytes = ((size_t)(k.b.n_scans > 0 ? k.b.n_scans : 1) * 625 * 4 + 255) & ~(size_t)255;
-    // the resolve on its own stream (one launch): the draws live in the slot, so the next call's
-    // resolve does not overwrite the ones this call's consensus still reads
-    k.res_side = c->resolve_stream && !k.b.draws_out && k.ep_count == 1;
-    const size_t dbytes = k.res_side ? (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4 : 0;
-    if (c->pslot_bytes < jbytes + sbytes + dbytes) {
+    if (c->pslot_bytes < jbytes + sbytes) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipStreamSynchronize(c->pstream));
-        HIPCHK(hipStreamSynchronize(c->rstream));
-        for (int i = 0; i < 3; i++) {
+        for (int i = 0; i < NSLOTS; i++) {
             if (c->pslot[i]) HIPCHK(hipFree(c->pslot[i]));
             c->pslot[i] = nullptr;
         }
         c->pslot_bytes = 0;
-        for (int i = 0; i < c->nslots; i++) {
-            hipError_t e = hipMalloc(&c->pslot[i], jbytes + sbytes + dbytes);
+        for (int i = 0; i < NSLOTS; i++) {
+            hipError_t e = hipMalloc(&c->pslot[i], jbytes + sbytes);
             if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (producer slot)");
             HIPCHK(e);
         }
-        c->pslot_bytes = jbytes + sbytes + dbytes;
+        c->pslot_bytes = jbytes + sbytes;
         c->spec_ok = 0;  // the previous producer's end state went with the old slots
     }
     k.jbuf = (unsigned char *)c->pslot[slot] + JBUF_FRONT;
@@ -3804,8 +3452,6 @@ static int prepare_steps(lslam_ctx *c, KArgs &k, int slot) {
     k.slot_jbytes = jbytes;
     if (k.b.draws_out) {
         k.draws_scr = k.b.draws_out;
-    } else if (k.res_side) {
-        k.draws_scr = (int32_t *)((unsigned char *)c->pslot[slot] + jbytes + sbytes);
     } else {
         int st = ensure_scratch(c, (size_t)(k.b.n_chunks > 0 ? k.b.n_chunks : 1) * 2 * (k.T + 1) * 4);
         if (st) return st;
@@ -3825,32 +3471,20 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     const int64_t need = ((int64_t)De * (N - 1) * esz + 46) & ~(int64_t)15;  // + alignment skew
     const int lds = need <= 16 * 1024 ? (int)need : 0;
     k.res_g = lds;  // staging capacity in bytes
-    if (lds == 0 && c->resolve_walk) {  // steps streamed from HBM, waves over (chunk, draw)
+    if (lds == 0) {  // steps streamed from HBM, waves over (chunk, draw)
         const int64_t items = (int64_t)k.b.n_chunks * De;
         // beside the next epoch's producer (produce_draws): two waves per SIMD, so its parsers
-        // keep their residency (three per SIMD displaced them: C5 107 vs 78 ms per call)
-        const int64_t cap = (k.ep_count > 1 && !c->epoch_serial) ? 8 * (int64_t)c->n_cus : (1 << 20);
+        // keep their residency (three per SIMD displaced them: C5 107 vs 78 ms per call).
+        // (Measured and dropped: LDS tiles of [64 draws][128 steps], 1.0 vs 0.43 ms per epoch.)
+        const int64_t cap = k.ep_count > 1 ? 8 * (int64_t)c->n_cus : (1 << 20);
         const dim3 grid(launch_cap(c, items > cap ? cap : items)), block(64);
         if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, rs, k);
         else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, rs, k);
         HIPCHK(hipGetLastError());
         return LSLAM_OK;
     }
-    if (lds == 0) {  // steps streamed through LDS tiles, waves over (chunk, 64 draws)
-        const int ngroups = (De + 63) / 64;
-        const int64_t items = (int64_t)k.b.n_chunks * ngroups;
-        const dim3 grid(launch_cap(c, items > (1 << 30) ? (1 << 30) : items)), block(64);
-        const int tl = 64 * (RB + 4) * esz;
-        if (k.j8) hipLaunchKernelGGL(resolve_big_kernel<uint8_t>, grid, block, tl, rs, k, ngroups);
-        else hipLaunchKernelGGL(resolve_big_kernel<uint16_t>, grid, block, tl, rs, k, ngroups);
-        HIPCHK(hipGetLastError());
-        return LSLAM_OK;
-    }
-    if (k.j8 && c->resolve_reg && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
-        if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg == 3) {
-            const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 127) / 128))), block(64);
-            hipLaunchKernelGGL(resolve_reg8x2_kernel, grid, block, 0, rs, k);
-        } else if (N - 1 <= 16 * RR_GROUPS - 1 && c->resolve_reg != 2) {
+    if (k.j8 && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
+        if (N - 1 <= 16 * RR_GROUPS - 1) {
             const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 63) / 64))), block(64);
             hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, rs, k);
         } else {
@@ -3876,35 +3510,18 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
     k.rt_all = c->rt_all;
     int lds = 0;
-    const int ppw = c->rng_ppw;
-    int st = layout_rng(k, &k.b, lds, ppw);
+    int st = layout_rng(k, &k.b, lds);
     if (st) return st;
-    // at least this much LDS per producer workgroup (LSLAM_RNG_LDS_MIN): above 32 KiB a CU holds
-    // at most 4 of them, so a workgroup that finds its CU busy waits for it instead of landing
-    // as a fifth on another CU (5 parsers per SIMD there: the whole launch 20-30 % longer)
-    static const int lds_min = [] { const char *e = getenv("LSLAM_RNG_LDS_MIN"); return e ? atoi(e) : 0; }();
-    if (lds < lds_min && lds_min <= 160 * 1024) lds = lds_min;
     static std::once_flag once;
     std::call_once(once, [] {
-        set_max_lds(rng_kernel<uint8_t, 1>);
-        set_max_lds(rng_kernel<uint16_t, 1>);
-        set_max_lds(rng_kernel<uint8_t, 4>);
-        set_max_lds(rng_kernel<uint16_t, 4>);
+        set_max_lds(rng_kernel<uint8_t>);
+        set_max_lds(rng_kernel<uint16_t>);
     });
     st = timer_begin(c, LSLAM_K_RNG, stream);
     if (st) return st;
-    // No helper wave by default: each parser twists its own next block when it needs it (its chain
-    // ~3 % longer), so the producer holds 4 instead of 5 waves per SIMD and the consumers beside it
-    // one more: C3 0.855 -> 0.839 ms per step.  LSLAM_RNG_SELF=0: the helper wave twists ahead.
-    static const bool self_tw = [] { const char *e = getenv("LSLAM_RNG_SELF"); return !(e && atoi(e) == 0); }();
-    const dim3 grid((unsigned)((k.b.n_scans + ppw - 1) / ppw)), block(64 * (ppw + (self_tw ? 0 : 1)));
-    if (ppw == 4) {
-        if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t, 4>), grid, block, lds, stream, k);
-        else hipLaunchKernelGGL((rng_kernel<uint16_t, 4>), grid, block, lds, stream, k);
-    } else {
-        if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t, 1>), grid, block, lds, stream, k);
-        else hipLaunchKernelGGL((rng_kernel<uint16_t, 1>), grid, block, lds, stream, k);
-    }
+    const dim3 grid((unsigned)((k.b.n_scans + RNG_PPW - 1) / RNG_PPW)), block(64 * RNG_PPW);
+    if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t>), grid, block, lds, stream, k);
+    else hipLaunchKernelGGL((rng_kernel<uint16_t>), grid, block, lds, stream, k);
     HIPCHK(hipGetLastError());
     return timer_end(c, LSLAM_K_RNG, stream);
 }
@@ -3918,13 +3535,7 @@ static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint3
     const int D = k.T + 1;
     // An epoch's resolve (the lane walk on a grid of two waves per SIMD) runs on the ctx
     // stream beside the next epoch's producer on ps, the slots alternating (C5: 78 vs 89 ms
-    // per call serial).  The LDS-tiled resolve slowed the parsers more than it hid (129 vs
-    // 112 ms): with it, or LSLAM_EPOCH_SERIAL=1, the epochs run one after the other.
-    if (k.ep_count > 1 && ps != c->stream && (c->epoch_serial || !c->resolve_walk)) {
-        HIPCHK(hipEventRecord(c->ev_produced, ps));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
-        ps = c->stream;
-    }
+    // per call with the epochs one after the other).
     const uint32_t *prev_state = nullptr;
     int sl = slot;
     for (int e = 0; e < k.ep_count; e++) {
@@ -3943,27 +3554,16 @@ static int produce_draws(lslam_ctx *c, KArgs &k, int slot, hipStream_t ps, uint3
         ke.b.mt_state_out = (last && final_out) ? final_out : ke.state_scr;
         int st = launch_rng(c, ke, ps);
         if (st) return st;
-        if (ps != c->stream && k.res_side) {
-            // resolve stream: after the producer, off the ctx chain; the ctx stream waits for it
-            // before the consensus
+        if (ps != c->stream) {
             HIPCHK(hipEventRecord(c->ev_produced, ps));
-            HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_produced, 0));
-            st = launch_resolve(c, ke, c->rstream);
-            if (st) return st;
-            HIPCHK(hipEventRecord(c->ev_resolved, c->rstream));
-            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_resolved, 0));
-        } else {
-            if (ps != c->stream) {
-                HIPCHK(hipEventRecord(c->ev_produced, ps));
-                HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
-            }
-            st = launch_resolve(c, ke, c->stream);
-            if (st) return st;
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_produced, 0));
         }
+        st = launch_resolve(c, ke, c->stream);
+        if (st) return st;
         if (!last) HIPCHK(hipEventRecord(c->ev_slot_free[sl], c->stream));
         prev_state = ke.state_scr;
         last_slot = sl;
-        sl = (sl + 1) % c->nslots;
+        sl = (sl + 1) % NSLOTS;
     }
     k.state_scr = const_cast<uint32_t *>(prev_state);
     c->next_slot = sl;
@@ -4174,11 +3774,8 @@ static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
         set_max_lds(scan_kernel<LSLAM_HYP_EXPLICIT, MODE>);
         set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
-    static const bool w4 = [] { const char *e = getenv("LSLAM_POST_W4"); return e && atoi(e) != 0; }();
-    static const int post_cap = [] { const char *e = getenv("LSLAM_POST_CAP"); return e ? atoi(e) : 0; }();
-    const int64_t cap = post_cap > 0 && k.hyp_source == LSLAM_HYP_MT19937 ? (int64_t)post_cap * 4 * c->n_cus : k.b.n_scans;
-    const dim3 grid(launch_cap(c, std::min<int64_t>(k.b.n_scans, cap)));
-    if (k.hyp_source == LSLAM_HYP_MT19937 && !w4)  // beside the next call's producer
+    const dim3 grid(launch_cap(c, k.b.n_scans));
+    if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     else
         hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
@@ -4205,19 +3802,20 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (mt) {
         st = prepare_steps(c, k, slot);
         if (st) return st;
-        c->next_slot = (c->next_slot + 1) % c->nslots;
+        c->next_slot = (c->next_slot + 1) % NSLOTS;
     }
     KArgs kp;
     int lds_post = 0;
     // a UKF step that reads nothing of this call's RANSAC (no LMK_FROM_RANSAC / MAP) runs
     // on the side stream, off the resolve -> consensus -> association chain
     // (Philox / explicit hypotheses only: beside the MT producer a third stream of UKF waves
-    // slows the resolve -> consensus chain more than it saves, 1.23 -> 1.27-1.32 ms on C3)
-    const bool ukf_side = (p->hyp_source != LSLAM_HYP_MT19937 || c->ukf_side_mt) && u &&
+    // slows the resolve -> consensus chain more than it saves, 1.23 -> 1.27-1.32 ms on C3, and
+    // made the step bimodal)
+    const bool ukf_side = p->hyp_source != LSLAM_HYP_MT19937 && u &&
                           !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
     // the UKF of the fused call on lane groups after the association pass (not in MAP mode,
     // whose measurements come out of the association walk itself)
-    const bool ukf_lane = u && !ukf_side && !(u->flags & LSLAM_UKF_MAP) && c->ukf_lanes;
+    const bool ukf_lane = u && !ukf_side && !(u->flags & LSLAM_UKF_MAP);
     const int pmode = (assoc ? MODE_ASSOC : MODE_POST) | (u && !ukf_side && !ukf_lane ? MODE_UKF : 0);
     if (assoc || (u && !ukf_side && !ukf_lane)) {
         st = build_args(kp, b, p, (ukf_side || ukf_lane) ? nullptr : u, pmode, lds_post);
@@ -4244,14 +3842,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         if ((st = mark_calls(c))) return st;
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_call, 0));
         HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_copy, 0));
-        if (c->ukf_lanes) {
-            launch_ukf_group(ku, u->n_landmarks, c->ustream, false);
-        } else {
-            static std::once_flag once;
-            std::call_once(once, [] { set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>); });
-            hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE_UKF>), dim3(launch_cap(c, b->n_scans)), dim3(64),
-                               lds_u, c->ustream, ku);
-        }
+        launch_ukf_group(ku, u->n_landmarks, c->ustream, false);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev_ukf, c->ustream));
     }
@@ -4281,10 +3872,10 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         spec = hz == 1 && c->speculate && c->spec_ok && k.ep_count == 1 && c->prev_state_scr &&
                c->prev_spec_scans == b->n_scans && b->mt_state_in == c->prev_state_out && !state_copied;
         // a scan replayed by a speculative call stays dirty in every later one (its producer state
-        // is never repaired): every LSLAM_SPEC_RESYNC-th chained call (default 32)
-        // waits for the previous fix-up instead, which clears the flags
-        static const int spec_resync = [] { const char *e = getenv("LSLAM_SPEC_RESYNC"); const int v = e ? atoi(e) : 32; return v > 0 ? v : 32; }();
-        if (spec && ++c->spec_run >= spec_resync) spec = false;
+        // is never repaired): every SPEC_RESYNC-th chained call waits for the
+        // previous fix-up instead, which clears the flags (test_gpu_speculate.py runs past it)
+        constexpr int SPEC_RESYNC = 32;
+        if (spec && ++c->spec_run >= SPEC_RESYNC) spec = false;
         if (!spec) c->spec_run = 0;
         if (hz == 1 && !spec) HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[c->prev_slot], 0));
         // a producer that waited on the previous call will most likely wait on this one too, so
@@ -4298,29 +3889,15 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         k.b.mt_state_in = true_in;  // the fix-up's replays start from the true state
         if (st) return st;
     }
-    // a UKF that reads nothing of this call's RANSAC may run anywhere in the ctx chain
-    // (LSLAM_UKF_EARLY: 0 after the post pass, 1 before the fix-up, 2 before the consensus,
-    // 3 = default: between the fix-up and the post pass).  The fix-up releases this call's
-    // steps slot; the next producer starts ~40 us after that event, so a UKF placed right
-    // behind the fix-up runs alone (35 us) instead of beside the parsers (~180 us): C3
-    // 0.893 -> 0.858 ms per step, the producer 0.79 -> 0.71 ms in the pipeline
-    static const int ukf_early = [] { const char *e = getenv("LSLAM_UKF_EARLY"); return e ? atoi(e) : 3; }();
-    // where the slot's release event (the next producer's start) goes in the ctx chain
-    // (LSLAM_SLOT_AT): 0 = right after the fix-up (default), 1 = after the post pass (before a
-    // UKF placed after it), 2 = at the end of the call
-    static const int slot_at = [] { const char *e = getenv("LSLAM_SLOT_AT"); return e ? atoi(e) : 0; }();
+    // A UKF that reads nothing of this call's RANSAC runs between the fix-up and the post pass.
+    // The fix-up releases this call's steps slot; the next producer starts ~40 us after that
+    // event, so a UKF placed right behind the fix-up runs alone (35 us) instead of beside the
+    // parsers (~180 us): C3 0.893 -> 0.858 ms per step, the producer 0.79 -> 0.71 ms in the
+    // pipeline.  (Measured and dropped, DESIGN.md §8: the UKF before the fix-up, +2.7 %, or
+    // before the consensus, +0.8 %; the slot released after the post pass or at the call's end.)
     const bool ukf_indep = ukf_lane && !(u->flags & (LSLAM_UKF_LMK_FROM_RANSAC | LSLAM_UKF_MAP));
-    const int ukf_at = ukf_indep ? ukf_early : 0;
-    if (ukf_lane && ukf_at == 2) {
-        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
-        HIPCHK(hipGetLastError());
-    }
     st = launch_chunks(c, k, !assoc);
     if (st) return st;
-    if (ukf_lane && ukf_at == 1) {
-        launch_ukf_group(kl, u->n_landmarks, c->stream, true);
-        HIPCHK(hipGetLastError());
-    }
     if (mt) {
         KArgs kf = k;
         kf.fixup = 1;
@@ -4350,9 +3927,9 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_MT19937, MODE_RANSAC>), dim3(launch_cap(c, b->n_scans)), dim3(64), lds_fix,
                            c->stream, kf);
         HIPCHK(hipGetLastError());
-        if (slot_at != 1 && slot_at != 2) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
+        HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     }
-    if (ukf_lane && ukf_at == 3) {
+    if (ukf_indep) {
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
         HIPCHK(hipGetLastError());
     }
@@ -4373,13 +3950,11 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         default: break;
     }
     if (st) return st;
-    if (mt && slot_at == 1) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
-    if (ukf_lane && ukf_at == 0) {
+    if (ukf_lane && !ukf_indep) {  // reads this call's chunk models (LMK_FROM_RANSAC)
         launch_ukf_group(kl, u->n_landmarks, c->stream, true);
         HIPCHK(hipGetLastError());
     }
     if (ukf_side) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_ukf, 0));
-    if (mt && slot_at == 2) HIPCHK(hipEventRecord(c->ev_slot_free[slot], c->stream));
     remember_outputs(c, b, k.T, u ? u->n_landmarks : 0);
     if ((st = end_call(c))) return st;
     return timer_end(c, LSLAM_K_PIPELINE);
@@ -4456,7 +4031,7 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     const int slot = c->next_slot;
     st = prepare_steps(c, k, slot);
     if (st) return st;
-    c->next_slot = (c->next_slot + 1) % c->nslots;
+    c->next_slot = (c->next_slot + 1) % NSLOTS;
     st = timer_begin(c, LSLAM_K_HYP);
     if (st) return st;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_slot_free[slot], 0));
@@ -4510,11 +4085,11 @@ static int ukf_step_impl(lslam_ctx *c, const lslam_scan_batch *b, const lslam_uk
     if (!bb.scan_chunk_off) return set_err(LSLAM_ERR_ARG, "scan_chunk_off required (may describe 0 chunks)");
     int st = build_args(k, &bb, nullptr, u, MODE_UKF, lds);
     if (st) return st;
-    const bool lanes = c->ukf_lanes && !(u->flags & LSLAM_UKF_MAP);
+    const bool lanes = !(u->flags & LSLAM_UKF_MAP);  // MAP: the one-wave form (its post pass's step)
     if ((u->flags & LSLAM_UKF_SIGMAS_IN) && !b->ukf_sigmas)
         return set_err(LSLAM_ERR_ARG, "LSLAM_UKF_SIGMAS_IN without ukf_sigmas");
     if ((b->ukf_sigmas || trace) && !lanes)
-        return set_err(LSLAM_ERR_UNSUPPORTED, "ukf_sigmas / trace need the lane-group UKF (not MAP, LSLAM_UKF_LANES != 0)");
+        return set_err(LSLAM_ERR_UNSUPPORTED, "ukf_sigmas / trace need the lane-group UKF (not LSLAM_UKF_MAP)");
     if (trace && !(u->flags & LSLAM_UKF_UPDATE)) return set_err(LSLAM_ERR_ARG, "lslam_ukf_trace needs LSLAM_UKF_UPDATE");
     if (trace || b->ukf_sigmas) {
         HIPCHK(hipSetDevice(c->device));

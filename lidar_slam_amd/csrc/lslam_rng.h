@@ -58,15 +58,10 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 // v_bfe_i32, (mask & MATRIX_A) ^ far as one v_bitop3, the shift, the xor (the plain form
 // compiles to seven).
 __device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far) {
-#ifndef LSLAM_MIX7
     const uint32_t y = __builtin_amdgcn_bitop3_b32(cur, nxt, MT_LO, 0xD8);
     const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)nxt, 0, 1);
     const uint32_t t = __builtin_amdgcn_bitop3_b32(m, MT_MA, far, 0x6A);
     return t ^ (y >> 1);
-#else
-    uint32_t y = (cur & MT_UP) | (nxt & MT_LO);
-    return far ^ (y >> 1) ^ ((y & 1u) ? MT_MA : 0u);
-#endif
 }
 
 // mt19937_gen on key[624] in LDS by one wave

@@ -15,11 +15,8 @@
 //   blocks:           block b+1 of the MT state is twisted out of place into the
 //                     other of two 624-word slots of raw state (then a 64-word
 //                     pad holding slot 0's head, so a window may run across the
-//                     block boundary).  By default the parser twists it itself
-//                     when it first needs it (rp_need_block: one producer wave
-//                     per SIMD fewer beside the consumers); with
-//                     LSLAM_RNG_SELF=0 a helper wave per workgroup twists ahead
-//                     and sleeps until a parser's s_wakeup (rng_kernel).
+//                     block boundary) by the parser itself, when it first needs
+//                     it (rp_need_block).
 // Turning the steps into the two drawn indices is bulk, data-parallel work
 // (resolve_chunk below); it runs in the consensus kernel, one wave per chunk,
 // where all of a chunk's draws are resolved together.
@@ -31,7 +28,7 @@
 
 namespace lslam {
 
-enum { F_BLK = 0, F_BLKUSE = 1, F_NFLAGS = 8 };
+enum { F_BLK = 0, F_NFLAGS = 8 };
 
 // flags are LDS words: keep the address space explicit, or a volatile access
 // through a generic pointer becomes a system-coherent FLAT load/store
@@ -44,10 +41,6 @@ __device__ __forceinline__ void lds_flag_put(lds_flag_t *f, int v) {
     *f = v;
     asm volatile("" ::: "memory");
 }
-
-// A wakeup that arrives while the helper is still awake is lost; its sleep
-// then simply runs out (s_sleep 127 ~ 8k cycles).
-__device__ __forceinline__ void wake_helper() { asm volatile("s_wakeup" ::: "memory"); }
 
 // Waves of a SIMD issue by priority, then age.  With equal priorities the
 // oldest parser of a SIMD races ahead and the youngest finishes last.
@@ -132,7 +125,6 @@ struct RngPipe {
     uint32_t lvl_t1, lvl_t2;  // parser: done steps at which the level drops (rp_set_schedule)
     uint32_t done_steps;   // parser: steps of the finished chunks
     int prio;              // parser: current priority level
-    bool self_twist;       // no helper wave: the parser twists each block itself when it needs it
 #ifdef LSLAM_STAMPS
     uint64_t acc[8];
 #endif
@@ -151,22 +143,20 @@ __device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done) {
     return RP_PRIO_TOP - (done >= rp.lvl_t1 ? 1 : 0) - (done >= rp.lvl_t2 ? 1 : 0);
 }
 
-// Block `need` of the pipe, before the parser reads it: from the helper wave (its flag), or
-// twisted by the parser itself (self_twist: block need - 1 -> slot need & 1, which held block
-// need - 2, already parsed; an even block also refreshes the pad after slot 1).
+// Block `need` of the pipe, before the parser reads it: twisted by the parser itself (block
+// need - 1 -> slot need & 1, which held block need - 2, already parsed; an even block also
+// refreshes the pad after slot 1).  F_BLK = the newest block in the pipe.  (A helper wave per
+// workgroup that twisted ahead was measured and dropped at r03: the parsers' chains got ~3 %
+// shorter, but the producer then held 5 instead of 4 waves per SIMD, one consumer wave fewer.)
 __device__ __forceinline__ void rp_need_block(RngPipe &rp, int need, int lane) {
-    if (rp.self_twist) {
-        if (lds_flag_get(rp.fl + F_BLK) < need) {
-            mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N, lane);
-            if ((need & 1) == 0) {
-                rp.blk[2 * MT_N + lane] = rp.blk[lane];
-                wave_lds_sync();
-            }
-            lds_flag_put(rp.fl + F_BLK, need);
+    if (lds_flag_get(rp.fl + F_BLK) < need) {
+        mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N, lane);
+        if ((need & 1) == 0) {
+            rp.blk[2 * MT_N + lane] = rp.blk[lane];
+            wave_lds_sync();
         }
-        return;
+        lds_flag_put(rp.fl + F_BLK, need);
     }
-    while (lds_flag_get(rp.fl + F_BLK) < need) __builtin_amdgcn_s_sleep(1);
 }
 
 // Diagnostic build only: parser cycle accounting (0 block waits, 2 fixed point,
@@ -266,10 +256,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            if (!rp.self_twist) {
-                lds_flag_put(rp.fl + F_BLKUSE, blkno);
-                wake_helper();
-            }
             const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;
@@ -378,17 +364,12 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
 // M << s.  Accepted lanes store v at step g + a_l; the consumer applies
 // mask(i) itself (v & mask(i) = the step's j), so no per-lane i is formed here.
 
-// LSLAM_REJ32 (default): the sign test reads the shifted window's high dword only (an empty asm
-// keeps the compiler from folding it back into a 64-bit compare of the whole shift).  A/B at r04:
-// C3 0.785 vs 0.804 ms per step, producer 0.737 vs 0.749 ms (2 x 2 runs, one box)
-#ifndef LSLAM_REJ32
-#define LSLAM_REJ32 1
-#endif
+// The sign test reads the shifted window's high dword only (an empty asm keeps the compiler
+// from folding it back into a 64-bit compare of the whole shift).  A/B at r04: C3 0.785 vs
+// 0.804 ms per step, producer 0.737 vs 0.749 ms (2 x 2 runs, one box).
 __device__ __forceinline__ bool rt_rej(uint64_t M, uint32_t s) {
     uint32_t hi = (uint32_t)((M << s) >> 32);
-#if LSLAM_REJ32
     asm("" : "+v"(hi));
-#endif
     return (int32_t)hi < 0;
 }
 
@@ -401,15 +382,6 @@ __device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
         while (x >= K) x -= K;
     return x;
 }
-
-
-// evaluations after the first one before the first convergence check (tbl_window)
-#ifndef LSLAM_TBL_UNCHECKED
-#define LSLAM_TBL_UNCHECKED 2
-#endif
-#ifndef LSLAM_TBL_ASM
-#define LSLAM_TBL_ASM 1  // a table window's evaluations, checked turns and store as one asm block (0: the compiler's form, A/B)
-#endif
 
 typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
 __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
@@ -424,21 +396,31 @@ __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, u
     return ((uint64_t)hi << 32) | lo;
 }
 
-// the table for K from the library's global copy (rt_all[K-2]) into the pipe
-__device__ __forceinline__ void rt_load(RngPipe &rp, const uint32_t *__restrict__ rt_all, uint32_t K, int lane) {
-    const uint32_t mK = 0xffffffffu >> __clz((int)K);
-    const uint4 *src = (const uint4 *)(rt_all + (size_t)(K - 2u) * RT_DWORDS);
-    uint4 *dst = (uint4 *)rp.tbl;
-    const uint32_t n4 = (mK + 1u) * RT_ST / 4u;  // rows 0..mK (mK + 1 >= 4, a power of two)
-    for (uint32_t e = (uint32_t)lane; e < n4; e += 64) dst[e] = src[e];
-    wave_lds_sync();
-    rp.tblK = K;
-}
-
 // One full table-mode window (64 words, short of the chunk's end).  Only the last window of a
 // run may run across the block's end (CHECK): the others skip that test, so the run loop
 // carries one backward branch per window.
 // gq = g + 63 (steps of the chunk before this window, + 63): lane l's step is gq - s_l.
+//
+// The fixed point: three evaluations (the first at the 0.72-accepts guess s0) without a
+// convergence check (a further evaluation of the fixed point leaves it unchanged; ~4.5 reach
+// it on average), then one per checked turn.  Two unchecked after the first measured fastest
+// at r04 (C3 step 0.777 vs 0.793 ms with three; one: 0.765-0.773 vs 0.761-0.769): the
+// producer's instruction count, not its checks' latency, is what the consumers beside it feel.
+// Measured and dropped: a count-based convergence test (6 VALU per checked turn), reading each
+// test one turn late (one evaluation more per window: 0.81 vs 0.77 ms).
+//
+// The product form is one asm block: the evaluations, the checked turns and the store.  The
+// checked turns keep the ballot in VCC and in s[40:41] in turn, so no turn copies the ballot
+// it compares against (the compiler's loop spends an s_mov_b64 per turn).  Both exits leave
+// the fixed point in VCC (equal to s[40:41]) and its counts in S; v[28:29] is the shift's
+// scratch pair.  Wait states (gfx950, tests/test_isa_hazards.py checks them in the built code
+// object): one between v_lshlrev_b64 and the v_cmp that reads its high dword (the compiler
+// puts the same s_nop 0 there: tools/hazard_probe.hip), two between a v_cmp writing VCC or an
+// SGPR pair and the v_mbcnt reading it as a lane mask (VALU SGPR write -> VALU read of that
+// SGPR as a constant: an s_nop 1, or the s_cmp + s_cbranch of a checked turn).  Nothing after
+// the exec restore reads EXEC as DPP data, so the block ends without a wait state (A/B at r04:
+// 0.765 vs 0.768 ms with a trailing s_nop).  The diagnostic stamp build (LSLAM_STAMPS) keeps
+// the compiler's form of the same iteration, cut into stamped segments.
 template <bool CHECK, bool KGE64, typename JT>
 __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int blkno, int &pos, uint32_t &raw,
                                            uint32_t &gq, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
@@ -475,19 +457,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     if (wst) asm volatile("" ::"v"((uint32_t)M), "v"((uint32_t)(M >> 32)));
 #endif
     WSTAMP(1);
-    // LSLAM_TBL_UNCHECKED evaluations after the first without a convergence check (one more
-    // evaluation of the fixed point leaves it unchanged; ~4.5 reach it on average), then one per
-    // check.  Two (three evaluations before the first check) measured fastest at r04 (C3 step
-    // 0.777 vs 0.793 ms with three): the producer's VALU count, not its checks' latency, is what
-    // the consumers beside it feel.  A count-based test (converged when mbcnt(R) repeats the
-    // counts, which needs no confirming evaluation) was slower: 6 VALU per checked turn.
-#if LSLAM_TBL_ASM && LSLAM_TBL_UNCHECKED == 2 && LSLAM_REJ32 && !defined(LSLAM_STAMPS) && !defined(LSLAM_TBL_LATECHECK)
-    // The evaluations, the checked turns and the store as one asm block: the checked turns keep
-    // the ballot in VCC and in s[40:41] in turn, so no turn copies the ballot it compares against
-    // (the compiler's loop spends an s_mov_b64 per turn).  Wait states: one between the 64-bit
-    // shift and the compare of its high dword, two between a compare's mask and the v_mbcnt that
-    // reads it (an s_nop 1, or the s_cmp + s_cbranch of a turn).  Both exits leave the fixed
-    // point in VCC (equal to s[40:41]) and its counts in S.  v[28:29] is the shift's scratch pair.
+#ifndef LSLAM_STAMPS
     uint32_t na, tS, tI;
     uint64_t tE;
 #define TBL_EVAL_VCC                                \
@@ -497,13 +467,6 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
     "s_nop 0\n\t"                                 \
     "v_cmp_gt_i32_e32 vcc, 0, v29\n\t"            \
     "s_nop 1\n\t"
-// No s_nop after the exec restore: no VALU that reads EXEC as data (DPP) follows the block (A/B
-// with LSLAM_TBL_ASM_TAILNOP: 0.765 vs 0.768 ms, 4 x 2 runs; 91 GPU tests green without it)
-#ifdef LSLAM_TBL_ASM_TAILNOP
-#define TBL_TAIL_NOP "\n\ts_nop 0"
-#else
-#define TBL_TAIL_NOP ""
-#endif
 #define TBL_TURNS                                                   \
     "v_lshlrev_b64 v[28:29], %[s0], %[M]\n\t"                     \
     "s_nop 0\n\t"                                                 \
@@ -531,7 +494,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
                      "s_andn1_saveexec_b64 %[E], vcc\n\t"
                      "global_store_byte %[I], %[v], %[J]\n\t"
                      "s_mov_b64 exec, %[E]\n\t"
-                     "s_bcnt0_i32_b64 %[na], vcc" TBL_TAIL_NOP
+                     "s_bcnt0_i32_b64 %[na], vcc"
                      : [na] "=s"(na), [S] "=&v"(tS), [I] "=&v"(tI), [E] "=&s"(tE)
                      : [M] "v"(M), [s0] "v"(s0), [sb] "v"(sbase), [v] "v"(v), [gq] "s"(gq), [J] "s"(J)
                      : "vcc", "scc", "v28", "v29", "s40", "s41", "memory");
@@ -541,50 +504,23 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
                      "s_andn1_saveexec_b64 %[E], vcc\n\t"
                      "global_store_short %[I], %[v], %[J]\n\t"
                      "s_mov_b64 exec, %[E]\n\t"
-                     "s_bcnt0_i32_b64 %[na], vcc" TBL_TAIL_NOP
+                     "s_bcnt0_i32_b64 %[na], vcc"
                      : [na] "=s"(na), [S] "=&v"(tS), [I] "=&v"(tI), [E] "=&s"(tE)
                      : [M] "v"(M), [s0] "v"(s0), [sb] "v"(sbase), [v] "v"(v), [gq] "s"(gq), [J] "s"(J)
                      : "vcc", "scc", "v28", "v29", "s40", "s41", "memory");
     }
 #undef TBL_TURNS
 #undef TBL_EVAL_VCC
-#undef TBL_TAIL_NOP
 #else
     uint64_t R = ballot(rt_rej(M, s0));
 #pragma unroll
-    for (int e = 0; e < LSLAM_TBL_UNCHECKED; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
+    for (int e = 0; e < 2; e++) R = ballot(rt_rej(M, mbcnt_from(R, sbase)));
 #ifdef LSLAM_WSTAMPS
     if (wst) asm volatile("" ::"s"(R));
 #endif
     WSTAMP(2);
     uint32_t s;
-    RP_COUNT(6, 1 + LSLAM_TBL_UNCHECKED);
-#ifdef LSLAM_TBL_LATECHECK
-    // The test of R_{k+1} == R_k reads the ballot one evaluation late: R_{k+2} is issued first,
-    // so the scalar compare finds R_{k+1}'s VALU result long done instead of waiting on it (the
-    // wait is most of a turn: ~140 of a window's ~760 cycles per checked turn, producer alone).
-    // One evaluation more per window (R_{k+2} = R_k once converged, discarded).  Three turns
-    // in a row rotate three ballots (ra, rb, rc) and their counts, so no turn copies a ballot
-    // that its own evaluation has just written.
-    uint64_t ra = R, rb, rc;
-    uint32_t sa = mbcnt_from(ra, sbase), sb, sc;
-    rb = ballot(rt_rej(M, sa));
-#define TBL_LATE_TURN(X, SX, Y, SY, Z, SZ)          \
-    SY = mbcnt_from(Y, sbase);                      \
-    Z = ballot(rt_rej(M, SY));                      \
-    __builtin_amdgcn_sched_barrier(0);              \
-    if (Y == X) {                                   \
-        R = X;                                      \
-        s = SX;                                     \
-        break;                                      \
-    }
-    for (;;) {
-        TBL_LATE_TURN(ra, sa, rb, sb, rc, sc)
-        TBL_LATE_TURN(rb, sb, rc, sc, ra, sa)
-        TBL_LATE_TURN(rc, sc, ra, sa, rb, sb)
-    }
-#undef TBL_LATE_TURN
-#else
+    RP_COUNT(6, 3);
     for (;;) {
         s = mbcnt_from(R, sbase);
         const uint64_t Rn = ballot(rt_rej(M, s));
@@ -595,7 +531,6 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
         if (Rn == R) break;
         R = Rn;
     }
-#endif
     RP_COUNT(5, 1);
     WSTAMP(3);
     store_accepted(J, gq - s, v, R);
@@ -632,10 +567,6 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            if (!rp.self_twist) {
-                lds_flag_put(rp.fl + F_BLKUSE, blkno);
-                wake_helper();
-            }
             const int lvl = rp_level(rp, rp.done_steps + g);
             if (lvl != rp.prio) {
                 rp.prio = lvl;

@@ -19,8 +19,9 @@ order.  The filterpy imports and the two unparseable functions are left out.  No
 the reference's text is stored: the archive holds inputs and outputs only, plus the
 sha256 and line span of each statement that ran (``meta_blocks``).
 
-Landmarks are reference ``landmarking.Landmark`` objects (landmarking.py:12-19;
-``transfer_function`` reads ``get_pos()``).  Poses are numpy float64 rows, as filterpy
+Landmarks are stand-ins for reference ``landmarking.Landmark`` objects holding what
+``transfer_function`` reads: ``get_pos()``, the ``np.array([x, y])`` of landmarking.py:17, :36-37
+(the reference module itself is not imported: only the ast-selected functions above run).  Poses are numpy float64 rows, as filterpy
 passes sigma points, so the angle arithmetic runs on np.float64 as it would in the UKF.
 
 Cases (S filters x L landmarks, inputs made with numpy's default_rng here):
@@ -51,7 +52,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.environ.get("LSLAM_GOLDEN_OUT", HERE)
 sys.path.insert(0, REF)
 
-import landmarking as lmk_ref  # noqa: E402  (reference, unmodified)
 
 WANT_DEFS = ("normalize_angle", "transfer_function", "residual_x", "residual_h")
 WANT_CONSTS = ("R", "L", "dt")
@@ -98,8 +98,20 @@ def load_reference_functions(path=os.path.join(REF, "UKFMethods.py")):
     return ns, ran
 
 
+class _Landmark:
+    """What transfer_function reads of a reference landmarking.Landmark: get_pos(), the
+    np.array([x, y]) the constructor stores (landmarking.py:17, :36-37).  A local stand-in, so
+    that no reference module runs beyond the ast-selected UKFMethods.py functions."""
+
+    def __init__(self, x, y):
+        self.pos = np.array([x, y])
+
+    def get_pos(self):
+        return self.pos
+
+
 def _landmarks(pts):
-    return [lmk_ref.Landmark(0.0, 0.0, j, float(px), float(py), float(px), float(py)) for j, (px, py) in enumerate(pts)]
+    return [_Landmark(float(px), float(py)) for px, py in pts]
 
 
 def edge_angles():

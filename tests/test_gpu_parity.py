@@ -391,19 +391,17 @@ def test_ukf_vs_oracle(ctx):
     _ukf_close(r["ukf_x"], r["ukf_P"], xo, Po)
 
 
-@pytest.mark.parametrize("L,lanes", [(20, "1"), (20, "0"), (4, "1")])
-def test_fused_ukf_landmarks_from_ransac_vs_oracle(ctx, L, lanes, monkeypatch):
+@pytest.mark.parametrize("L", [20, 4])
+def test_fused_ukf_landmarks_from_ransac_vs_oracle(ctx, L):
     """flags = PREDICT | UPDATE | LMK_FROM_RANSAC in the fused pipeline: landmark slot j of
     scan s becomes chunk j's fitted origin (Landmark.pos, ransac_functions.py:31) wherever that
     chunk is LSLAM_VALID, the rest keep ukf_lmk.  The kernel's (x, P) must equal the oracle's UKF
     run on exactly that substituted landmark set (1e-5 per component).  L = 4 < 8 chunks: only
-    the first L chunks feed slots.  Both UKF forms (lane groups, one wave per scan)."""
+    the first L chunks feed slots.  (The one-wave UKF form runs in map mode: test_gpu_map.py.)"""
     from lidar_slam_amd.pipeline import ScanPipeline
     from lidar_slam_amd import synth
     from lidar_slam_amd.device import Context
     from oracle import ukf as oukf
-    monkeypatch.setenv("LSLAM_UKF_LANES", lanes)  # read when a context is created
-    ctx = Context(0)
     ids = list(range(40))
     b = synth.make_batch(ids)
     S = len(ids)

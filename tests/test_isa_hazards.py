@@ -1,0 +1,212 @@
+"""The hand-placed wait states of the producer's asm table window, pinned to the compiler's own
+gfx950 hazard model (CPU test: needs hipcc and llvm-objdump, no GPU).
+
+``lslam_rng_pipe.h`` tbl_window issues the fixed-point evaluations of the table-mode parse
+(fit.py:819-826 behind ransac_functions.py:23-24: numpy's random_interval rejection) as one
+asm block, so the compiler's hazard recognizer does not see them; the block places its wait
+states by hand:
+
+  (A) one between ``v_lshlrev_b64 v[28:29]`` and the v_cmp that reads v29;
+  (B) two between a v_cmp writing VCC or s[40:41] and the v_mbcnt that reads it as a lane mask
+      (an ``s_nop 1``, or the ``s_cmp`` + ``s_cbranch`` of a checked turn).
+
+``tools/hazard_probe.hip`` writes the same evaluation chain in plain HIP (dependent and
+unrolled, so the scheduler has nothing to fill the gaps with): the wait states the compiler puts
+there are its requirement for gfx950.  This test reads them from the probe's assembly and then
+walks every control-flow path of the built library's ``rng_kernel`` (both step widths) from
+each such writer to its first VALU reader, checking that no path has fewer.  A toolchain or
+firmware change to these hazard rules then fails here, on the CPU, instead of as a rare wrong
+draw on the GPU.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(HIPCC) and os.path.exists(os.path.join(LLVM, "llvm-objdump"))),
+                                reason="needs hipcc and llvm-objdump")
+
+_REG = re.compile(r"(?<!\w)(v\[\d+:\d+\]|s\[\d+:\d+\]|[vs]\d+\b|vcc_lo\b|vcc_hi\b|vcc\b|exec\b)")
+
+
+def _regs(text):
+    """Registers named in an operand list, ranges expanded (vcc -> vcc_lo, vcc_hi)."""
+    out = set()
+    for r in _REG.findall(text):
+        m = re.match(r"([vs])\[(\d+):(\d+)\]", r)
+        if m:
+            out.update("%s%d" % (m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1))
+        elif r == "vcc":
+            out.update(("vcc_lo", "vcc_hi"))
+        else:
+            out.add(r)
+    return out
+
+
+class Insn:
+    def __init__(self, addr, mnem, ops, target=None):
+        self.addr, self.mnem, self.ops, self.target = addr, mnem, ops, target
+        parts = [p.strip() for p in ops.split(",")] if ops else []
+        self.dst = _regs(parts[0]) if parts else set()
+        self.src = set().union(*[_regs(p) for p in parts[1:]]) if len(parts) > 1 else set()
+        if mnem.startswith("v_cmp") and mnem.endswith("_e32"):  # VOPC: vcc is the implicit destination
+            self.src |= self.dst
+            self.dst = {"vcc_lo", "vcc_hi"}
+
+    @property
+    def wait(self):
+        m = re.match(r"s_nop\s+(\d+)", self.mnem + " " + self.ops)
+        return int(m.group(1)) + 1 if m else 1
+
+
+def _parse_s(text):
+    """Instructions of a compiler .s file, in order (labels and directives dropped)."""
+    out = []
+    for ln in text.splitlines():
+        ln = ln.split(";")[0].rstrip()
+        if not re.match(r"^\s+[sv]_", ln):
+            continue
+        f = ln.strip().split(None, 1)
+        out.append(Insn(len(out), f[0], f[1] if len(f) > 1 else ""))
+    return out
+
+
+def _parse_objdump(text, symbol):
+    """Instructions of one function of llvm-objdump -d output, with addresses and branch targets.
+    The asm block's local labels (TBLA_n / TBLX_n) appear as symbols inside the function."""
+    syms = {}
+    for ln in text.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.+)>:$", ln)
+        if m:
+            syms[m.group(2)] = int(m.group(1), 16)
+    lines = text.splitlines()
+    start = next(i for i, ln in enumerate(lines) if ln.endswith("<%s>:" % symbol))
+    out = []
+    for ln in lines[start + 1:]:
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", ln)
+        if m and not m.group(1).startswith("TBL"):
+            break  # the next function
+        m = re.match(r"^\s+(\S+)\s*(.*?)\s*//\s*([0-9A-F]+):", ln)
+        if not m:
+            continue
+        mnem, ops, addr = m.group(1), m.group(2), int(m.group(3), 16)
+        tgt = None
+        if mnem.startswith("s_cbranch") or mnem == "s_branch":
+            t = re.search(r"<([^+>]+)(?:\+0x([0-9a-f]+))?>", ln)
+            tgt = syms[t.group(1)] + (int(t.group(2), 16) if t.group(2) else 0) if t else None
+            ops = ""
+        out.append(Insn(addr, mnem, ops, tgt))
+    return out
+
+
+def _min_wait(insns, is_writer, regs_of, is_reader, need=None):
+    """Smallest number of wait states on any control-flow path from a writer to the first
+    instruction reading what it wrote (is_reader), over all writers; paths stop where the
+    registers are overwritten or `need` wait states have passed."""
+    index = {x.addr: i for i, x in enumerate(insns)}
+    best = None
+    for i, w in enumerate(insns):
+        if not is_writer(w):
+            continue
+        regs = regs_of(w)
+        stack, seen = [(i + 1, 0)], set()
+        while stack:
+            j, ws = stack.pop()
+            if j >= len(insns) or (j, ws) in seen:
+                continue
+            seen.add((j, ws))
+            x = insns[j]
+            if is_reader(x, regs):
+                best = ws if best is None else min(best, ws)
+                continue
+            if x.dst & regs and not x.mnem.startswith("s_cbranch"):
+                continue
+            if need is not None and ws >= need:
+                continue
+            if x.mnem in ("s_endpgm", "s_setpc_b64"):
+                continue
+            nws = ws + x.wait
+            if x.mnem == "s_branch":
+                if x.target in index:
+                    stack.append((index[x.target], nws))
+                continue
+            stack.append((j + 1, nws))
+            if x.mnem.startswith("s_cbranch") and x.target in index:
+                stack.append((index[x.target], nws))
+    return best
+
+
+def _shift_writer(x):
+    return x.mnem == "v_lshlrev_b64"
+
+
+def _shift_regs(x):
+    return {max(x.dst, key=lambda r: int(r[1:]))}  # the high dword
+
+
+def _valu_reads(x, regs):
+    return x.mnem.startswith("v_") and bool(x.src & regs)
+
+
+def _mbcnt_reads(x, regs):
+    return x.mnem.startswith("v_mbcnt") and bool(x.src & regs)
+
+
+def _mask_writer(x):
+    return x.mnem.startswith("v_cmp") and bool(x.dst & {"vcc_lo", "vcc_hi"} or any(r.startswith("s") for r in x.dst))
+
+
+def _mask_regs(x):
+    return set(x.dst)
+
+
+@pytest.fixture(scope="module")
+def probe_waits(tmp_path_factory):
+    d = tmp_path_factory.mktemp("probe")
+    out = str(d / "probe.s")
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", "-o", out,
+                           os.path.join(ROOT, "tools", "hazard_probe.hip")], stderr=subprocess.DEVNULL)
+    ins = _parse_s(open(out).read())
+    a = _min_wait(ins, _shift_writer, _shift_regs, _valu_reads)
+    b = _min_wait(ins, _mask_writer, _mask_regs, _mbcnt_reads)
+    assert a is not None and b is not None, "probe: evaluation chain not found"
+    return a, b
+
+
+@pytest.fixture(scope="module")
+def library_code(tmp_path_factory):
+    from lidar_slam_amd import build
+    lib = build.build(verbose=False)
+    d = tmp_path_factory.mktemp("lib")
+    so = str(d / "lib.so")
+    shutil.copy(lib, so)
+    subprocess.check_call([os.path.join(LLVM, "llvm-objdump"), "--offloading", so], cwd=str(d),
+                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    co = [f for f in os.listdir(str(d)) if "gfx950" in f]
+    assert co, "no gfx950 code object in the library"
+    return subprocess.check_output([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", str(d / co[0])],
+                                   text=True)
+
+
+def test_probe_matches_the_documented_rules(probe_waits):
+    """The compiler's requirement is what lslam_rng_pipe.h's comment states: (A) 1, (B) 2."""
+    assert probe_waits == (1, 2)
+
+
+@pytest.mark.parametrize("symbol", ["_Z10rng_kernelIhEv5KArgs", "_Z10rng_kernelItEv5KArgs"])
+def test_rng_kernel_asm_window_wait_states(probe_waits, library_code, symbol):
+    need_a, need_b = probe_waits
+    ins = _parse_objdump(library_code, symbol)
+    assert sum(x.mnem == "v_lshlrev_b64" for x in ins) >= 8, "asm table window not found"
+    # (paths stop once `need` wait states have passed: a writer whose every path is padded that
+    # far records nothing; the asm block's own pairs sit exactly at the bound)
+    a = _min_wait(ins, _shift_writer, _shift_regs, _valu_reads, need=need_a)
+    b = _min_wait(ins, _mask_writer, _mask_regs, _mbcnt_reads, need=need_b)
+    assert a == need_a, ("v_lshlrev_b64 -> VALU reader", a, need_a)
+    assert b == need_b, ("v_cmp mask -> v_mbcnt", b, need_b)

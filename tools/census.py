@@ -8,7 +8,7 @@ wave), how long they lived, how many were resident at once, and how the parsers 
 placed (parsers per SIMD, late workgroups).  The s_memrealtime clock is 100 MHz.
 
   python tools/census.py [--steps K] [--warmup W] [--scans S] [--out gpurun_out/census.npz]
-Environment knobs of the library (LSLAM_UKF_SIDE=1 ...) apply as usual.
+LSLAM_MT_SPECULATE=0 applies as usual.
 """
 import argparse
 import ctypes as C

@@ -1,0 +1,24 @@
+// Hazard probe (test infrastructure, not product): the table window's fixed-point evaluation
+// (lslam_rng_pipe.h tbl_window) written in plain HIP, so that the compiler's own gfx950 hazard
+// recognizer places the wait states.  tests/test_isa_hazards.py compiles this file to assembly,
+// reads the wait states the compiler put between (a) v_lshlrev_b64 and the first VALU reading
+// its result and (b) a v_cmp writing an SGPR pair and the v_mbcnt reading it as a lane mask,
+// and checks that the hand-scheduled asm block in the built library's rng_kernel has at least
+// as many at every such pair.  The chain is fully dependent and unrolled, so the scheduler has
+// nothing independent to fill them with: the compiler's s_nops are exactly its requirement.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+__global__ void hazard_probe(const uint64_t *Min, uint64_t *out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t M = Min[threadIdx.x];
+    uint64_t R = __ballot((int)(M >> 63));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t s = __builtin_amdgcn_mbcnt_hi((uint32_t)(R >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)R, 63u - lane));
+        uint32_t hi = (uint32_t)((M << s) >> 32);
+        asm("" : "+v"(hi));
+        R = __ballot((int32_t)hi < 0);
+    }
+    out[threadIdx.x] = R;
+}

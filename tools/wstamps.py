@@ -7,7 +7,7 @@ scans and prints, per window inside a run (tbl_window<false>, K = 99 and K = 19)
 cycles of each segment with the stamp's own cost (an empty segment) subtracted:
   temper      the next window's word load issued + temper of this window's words
   table       reject-table row read (LDS) + the two funnel shifts
-  unchecked   the first evaluation + LSLAM_TBL_UNCHECKED evaluations without a test
+  unchecked   the first evaluation + 2 evaluations without a test
   checked     the checked loop: one evaluation, VALU->SALU compare and branch per turn
   store       the accepted lanes' store, accepted count, step / position bookkeeping
 Stamps serialise the wave (s_memtime + s_waitcnt): read the segments as a latency
@@ -50,7 +50,7 @@ out["window_total_minus_stamps"] = round(sum(seg.values()), 1)
 out["stamp_cost"] = round(cal, 1)
 out["windows_per_scan"] = round(nwin / S, 1)
 out["checked_turns_per_window"] = round(w[:, 6].sum() / nwin, 3)
-out["unchecked_evals"] = 1 + int(os.environ.get("LSLAM_TBL_UNCHECKED", "3"))
+out["unchecked_evals"] = 3
 out["shares"] = {n: round(v / max(sum(seg.values()), 1e-9), 3) for n, v in seg.items()}
 out["parser_total_cycles_per_scan"] = round(float(dbg.download()[:, 7].astype(np.float64).mean()), 1)
 print(json.dumps(out))
