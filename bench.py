@@ -409,6 +409,14 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
     return res
 
 
+def rank_device(local_rank):
+    """The HIP device of this rank: LOCAL_RANK, or LSLAM_RANK_DEVICE for every rank when set (a
+    multi-rank rehearsal of the driver's N > 1 launch on a one-GPU box: all ranks on device 0).
+    Read before any HIP call."""
+    v = os.environ.get("LSLAM_RANK_DEVICE")
+    return int(v) if v not in (None, "") else int(local_rank)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -472,7 +480,7 @@ def main():
     from lidar_slam_amd.device import Context
     from lidar_slam_amd.pipeline import ScanPipeline
 
-    ctx = Context(local)
+    ctx = Context(rank_device(local))
     S = args.scans
     ids = shard_scan_ids(rank, S)
     b, ukf = make_workload(ids, args.beams, L, seed_base=rank)

@@ -1725,8 +1725,11 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
         }
     }
     __syncthreads();
+    // the claimed Ks, wave-uniform (SGPRs): the parser's table base then stays scalar, and a row's
+    // LDS address costs one VALU (rt_window)
+    const int kt0 = uni(kslot[0]), kt1 = uni(kslot[1]);
     for (int t = 0; t < 2; t++) {
-        const int K = kslot[t];
+        const int K = t ? kt1 : kt0;
         if (K == 0) continue;
         const uint32_t mK = 0xffffffffu >> __clz(K);
         const uint4 *src = (const uint4 *)(a.rt_all + (size_t)(K - 2) * RT_DWORDS);
@@ -1764,9 +1767,9 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
         if (N < 3) continue;
         JT *Jc = J + (size_t)D * (size_t)p0;
         const int K = N - 1;
-        const bool tbl = K <= (int)RT_KMAX && (kslot[0] == K || kslot[1] == K);
+        const bool tbl = K <= (int)RT_KMAX && (kt0 == K || kt1 == K);
         if (tbl) {
-            rp.tbl = stbl + (kslot[0] == K ? 0 : RT_DWORDS);
+            rp.tbl = stbl + (kt0 == K ? 0 : RT_DWORDS);
             rp.tblK = (uint32_t)K;
         }
         if (tbl && K >= 64) parse_chunk_tbl<true>(rp, blkno, pos, Jc, (uint32_t)N, D, lane);

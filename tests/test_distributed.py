@@ -65,3 +65,13 @@ def test_two_rank_sharding_barrier_and_max():
     full = orc.run_batch(b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], list(range(6)))[0]
     both = np.concatenate([np.frombuffer(m0, np.uint8), np.frombuffer(m1, np.uint8)])
     assert np.array_equal(both, full)
+
+
+def test_rank_device_override(monkeypatch):
+    """bench.py's device per rank: LOCAL_RANK, or LSLAM_RANK_DEVICE for every rank (the one-GPU
+    rehearsal of the driver's multi-rank launch, profiles/r05_rehearsal_2ranks.log)."""
+    import bench
+    monkeypatch.delenv("LSLAM_RANK_DEVICE", raising=False)
+    assert bench.rank_device(3) == 3
+    monkeypatch.setenv("LSLAM_RANK_DEVICE", "0")
+    assert bench.rank_device(3) == 0
