@@ -1896,7 +1896,7 @@ __global__ __launch_bounds__(64) void resolve_reg_kernel(const KArgs a) {
 // i at byte K - i); the lowest group may start up to 15 bytes before the row (the
 // previous row, or the slot's front pad JBUF_FRONT) and walks only i <= K.
 constexpr int RR_GROUPS = 8;  // K <= 127
-constexpr size_t JBUF_FRONT = 64;  // bytes of a producer slot before its steps
+constexpr size_t JBUF_FRONT = 128;  // bytes of a producer slot before its steps (resolve_reg8_kernel's loads)
 // One step of both trackers, c = (j == c) ? i : c.  The two trackers are independent
 // chains, so both compares are issued (masks in two SGPR pairs) before both selects; the
 // v_mov of i between them gives each select the two VALU wait states gfx950 requires
@@ -2002,29 +2002,59 @@ __device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_
     rr_walk_groups<0>(w, K, K >> 4, c0, c1);  // K >> 4 groups with all 16 steps <= K
 }
 
-__global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a) {
+// Invalid steps of a lane whose chunk is shorter than the wave's longest (packed waves, below):
+// group t holds steps 16t+1 .. 16t+16 at bytes 15 .. 0, so steps past the lane's K are the group's
+// low 16 - clamp(K - 16t, 0, 16) bytes; they get all their low 7 bits set, so the step's
+// extraction yields mask(i) >= i > either tracker: never a match.
+__device__ __forceinline__ void rr_poison(uint4 &w, uint32_t K, uint32_t t) {
+    const int cnt = min(max((int)K - 16 * (int)t, 0), 16);  // valid steps of the group
+    const int nbad = 16 - cnt;                                // its low nbad bytes
+    uint32_t *d = (uint32_t *)&w;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int nb = min(max(nbad - 4 * k, 0), 4);  // invalid bytes of dword k (from its low end)
+        d[k] |= (uint32_t)(0x7f7f7f7full & ((1ull << (8 * nb)) - 1ull));
+    }
+}
+
+// Lanes are (chunk, draw) items of the whole launch in chunk-major order, 64 consecutive items
+// per wave: a chunk's 101 draws no longer leave the second of its two waves 37 of 64 lanes,
+// and a draw the consensus never reads (draw T: skimage draws it after its last trial,
+// fit.py:826) is not resolved unless the caller asked for draws_out.  C3: 12.5 instead of 16
+// waves per scan.  A wave whose lanes' chunks differ in size walks the longest chunk's steps,
+// the shorter rows poisoned past their K (rr_poison).
+__global__ __launch_bounds__(64) void resolve_reg8_kernel(const KArgs a, int Dres) {
     const int lane = (int)threadIdx.x;
     const lslam_scan_batch &B = a.b;
     const uint32_t Dall = (uint32_t)a.T + 1u;
-    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;
-    const int ng = (int)((D + 63u) >> 6);  // waves per chunk: lanes = 64 draws
+    const uint32_t D = a.ep_nd > 0 ? (uint32_t)a.ep_nd : Dall;  // draws in the slot per chunk
     WAVE_CENSUS(a, WC_RESOLVE);
-    const int64_t total = (int64_t)B.n_chunks * ng;
-    for (int64_t e = blockIdx.x; e < total; e += gridDim.x) {
-        const int c = (int)(e / ng);
-        const uint32_t d = 64u * (uint32_t)(e - (int64_t)c * ng) + (uint32_t)lane;
+    const uint32_t total = (uint32_t)B.n_chunks * (uint32_t)Dres;  // < 2^31 (host)
+    for (uint32_t wb = blockIdx.x * 64u; wb < total; wb += gridDim.x * 64u) {
+        const uint32_t g = wb + (uint32_t)lane;
+        const bool live = g < total;
+        const int c = live ? (int)(g / (uint32_t)Dres) : 0;
+        const uint32_t d = live ? g - (uint32_t)c * (uint32_t)Dres : 0u;
         const int p0 = B.chunk_pt_off[c];
         const int N = B.chunk_pt_off[c + 1] - p0;
-        if (N < 3) continue;
-        const uint32_t K = (uint32_t)N - 1u;  // <= 127 (host)
-        const uint8_t *row = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)(d < D ? d : 0u) * K;
+        const bool act = live && N >= 3;
+        const uint32_t K = act ? (uint32_t)N - 1u : 0u;  // <= 127 (host)
+        const uint32_t kmax = (uint32_t)wave_max_dpp(act ? (int)K : 0);
+        const uint32_t kmin = (uint32_t)-wave_max_dpp(act ? -(int)K : INT_MIN + 1);
+        if (kmax < 2u) continue;
+        const uint8_t *row = (const uint8_t *)a.jbuf + (size_t)D * (size_t)p0 + (size_t)d * K;
         uint4 w[RR_GROUPS];
 #pragma unroll
         for (int t = 0; t < RR_GROUPS; t++)
-            if ((uint32_t)(16 * t) < K) w[t] = load16_unaligned(row + (int)K - 16 * (t + 1));
+            if ((uint32_t)(16 * t) < kmax) w[t] = load16_unaligned(row + (int)K - 16 * (t + 1));
+        if (kmin != kmax) {
+#pragma unroll
+            for (int t = 0; t < RR_GROUPS; t++)
+                if ((uint32_t)(16 * t) < kmax && (uint32_t)(16 * t + 16) > kmin) rr_poison(w[t], K, (uint32_t)t);
+        }
         uint32_t c0 = 0, c1 = 1;
-        rr_walk_row(w, K, c0, c1);
-        if (d < D) {
+        rr_walk_row(w, kmax, c0, c1);
+        if (act) {
             const uint32_t j1 = (w[0].w >> 24) & 1u;  // byte K - 1: step 1
             int32_t *draws = a.draws_scr + (size_t)c * 2 * Dall + 2 * (size_t)(a.ep_d0 + d);
             draws[0] = (int32_t)((j1 == 0u) ? c1 : c0);
@@ -3488,8 +3518,14 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     }
     if (k.j8 && c->resolve_beside) {  // no LDS: the producer's workgroups hold most of it
         if (N - 1 <= 16 * RR_GROUPS - 1) {
-            const dim3 grid(launch_cap(c, (int64_t)k.b.n_chunks * ((De + 63) / 64))), block(64);
-            hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, rs, k);
+            // draws of this launch to resolve per chunk: all but draw T (never read by the
+            // consensus) unless the caller wants the draws
+            const bool has_last = k.ep_d0 + De == k.T + 1;
+            const int Dres = (has_last && !k.b.draws_out && De > 1) ? De - 1 : De;
+            if ((int64_t)k.b.n_chunks * Dres >= ((int64_t)1 << 31) - 64)
+                return set_err(LSLAM_ERR_UNSUPPORTED, "more than 2^31 chunk draws in one call");
+            const dim3 grid(launch_cap(c, ((int64_t)k.b.n_chunks * Dres + 63) / 64)), block(64);
+            hipLaunchKernelGGL(resolve_reg8_kernel, grid, block, 0, rs, k, Dres);
         } else {
             const dim3 grid(launch_cap(c, k.b.n_chunks)), block(64);
             hipLaunchKernelGGL(resolve_reg_kernel, grid, block, 0, rs, k);
