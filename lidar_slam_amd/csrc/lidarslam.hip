@@ -433,36 +433,58 @@ __device__ __forceinline__ void count_one(double x, double y, double ux, double 
     asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
 }
 
-// one hypothesis per lane against all N points (gP: global, wave-uniform)
+// one hypothesis per lane against all N points (gP: global, wave-uniform).  Groups of 4 points
+// through two SGPR buffers in turn; the loop walks a pointer (two SALU per load) and tests it
+// once per 8 points (the index form spent ~15 SALU per 4 points on 64-bit address
+// arithmetic and two bounds tests).
 __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, double ux, double uy, double k,
                                                   cut_t r_lo, cut_t r_hi, int &lo, int &hi, double &S) {
-    int p = 0;
-    if (N >= 4) {
-        // two SGPR buffers in turn, so no copies between the load and its use
-        u32x16 A = sload_4pts(gP), B;
-        for (;;) {
-            swait(A);
-            const bool moreB = p + 8 <= N;
-            if (moreB) B = sload_4pts(gP + p + 4);
+    const double2 *q = gP;
+    if (N >= 8) {
+        // each buffer is waited on before the other one's load issues (scalar loads return out of
+        // order, so lgkmcnt(0) is the only wait); the last group of 8 is peeled so that the loop
+        // has one exit test at its bottom
+        const double2 *const qlast = gP + ((N >> 3) - 1) * 8;
+        u32x16 A = sload_4pts(q), B;
+        swait(A);
+        while (q != qlast) {
+            B = sload_4pts(q + 4);
             count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            p += 4;
-            if (!moreB) break;
             swait(B);
-            const bool moreA = p + 8 <= N;
-            if (moreA) A = sload_4pts(gP + p + 4);
+            A = sload_4pts(q + 8);
             count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(B[12], B[13]), sd(B[14], B[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            p += 4;
-            if (!moreA) break;
+            q += 8;
+            swait(A);
         }
+        B = sload_4pts(q + 4);
+        count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        swait(B);
+        count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(B[12], B[13]), sd(B[14], B[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        q += 8;
     }
-    for (; p < N; p++) {
-        u32x4 v = sload_pt(gP + p);
+    if (N & 4) {
+        u32x16 A = sload_4pts(q);
+        swait(A);
+        count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        q += 4;
+    }
+    for (int r = N & 3; r > 0; r--, q++) {
+        u32x4 v = sload_pt(q);
         swait(v);
         count_one(sd(v[0], v[1]), sd(v[2], v[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
     }
