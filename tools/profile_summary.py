@@ -40,13 +40,14 @@ KERNELS = {"rng_kernel": "rng_kernel", "resolve_reg": "resolve_reg", "resolve_ke
 
 
 def resolve_alg_bytes(beams, scans, trials):
-    """The resolve's algorithmic bytes per launch: every Fisher-Yates step read once (u8, chunks
-    <= 256 points: D = trials + 1 draws of K = N - 1 steps per chunk) + the draws written
-    (2 x int32 per draw)."""
+    """The resolve's algorithmic bytes per launch: every Fisher-Yates step of a resolved draw read
+    once (u8, chunks <= 256 points: K = N - 1 steps per draw) + the draws written (2 x int32 per
+    draw).  The bench passes no draws_out, so the resolve skips draw T (the one skimage makes
+    after the last trial): D = trials draws per chunk (D = 1 when trials = 0)."""
     sys.path.insert(0, ROOT)
     from lidar_slam_amd import synth
     sizes = synth.chunk_sizes(beams)
-    D = trials + 1
+    D = max(trials, 1)
     steps = sum(D * (n - 1) for n in sizes if n >= 3)
     draws = sum(D * 8 for n in sizes if n >= 3)
     return scans * steps, scans * draws
