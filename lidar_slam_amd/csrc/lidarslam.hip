@@ -2006,22 +2006,119 @@ __device__ __forceinline__ void rr_walk_group(const uint32_t (&ws)[4], uint32_t 
     }
 }
 
+// A full group (all 16 steps <= the wave's longest K) as SDWA byte compares: 4 VALU per step
+// instead of rr_step_nx's 5 (the byte extract goes) or rr_step's 6 (i > 64: no inline constant
+// for the select, so a v_mov of i).  Per dword of 4 steps one pre-op: steps i <= 64 mask their
+// bytes with mask(i) (one v_and with the 4 masks as a literal); steps i >= 65 all have mask 127
+// = the stored byte's own bound, and run in the XOR-64 domain: the bytes and the trackers are
+// XORed with 64 (a bijection on 0..127), so the select writes i ^ 64 = i - 64, an inline
+// constant 1..63.  The trackers enter that domain at group 4 and leave it after the last full
+// group (rr_walk_row).
+// Wait states (gfx950; checked on the built code object by tests/test_isa_hazards.py): two
+// between a v_cmp writing a mask SGPR pair and the v_cndmask reading it (the compiler's own
+// requirement, tools/hazard_probe.hip), and -- conservatively -- one between a v_cndmask and
+// the next SDWA compare, and between any VALU write of a VGPR and an SDWA read of it (the
+// compiler's SDWA compare/select chains put an s_nop 0 there in most but not all places).
+// Per step: cmp c0, cmp c1, F, select c0, select c1, G -- each compare two slots ahead of its
+// select, each select at least one slot ahead of the next SDWA compare.  F and G are the next
+// dwords' pre-ops where one is due, else s_nop 0 (waits inside dependency chains: ~free in
+// issue, profiles/r05_ubench_issue.json).
+#define RZ_CMP2(t, sel)                                                                  \
+    "v_cmp_eq_u32_sdwa %[mA], %[" t "], %[c0] src0_sel:BYTE_" sel " src1_sel:DWORD\n\t" \
+    "v_cmp_eq_u32_sdwa %[mB], %[" t "], %[c1] src0_sel:BYTE_" sel " src1_sel:DWORD\n\t"
+#define RZ_SEL2(k)                                               \
+    "v_cndmask_b32_e64 %[c0], %[c0], %[ib]+" k ", %[mA]\n\t" \
+    "v_cndmask_b32_e64 %[c1], %[c1], %[ib]+" k ", %[mB]\n\t"
+#define RZ_STEP(t, sel, k, F) RZ_CMP2(t, sel) F RZ_SEL2(k) RZ_NOP
+#define RZ_NOP "s_nop 0\n\t"
+#define RZ_AND(t, k) "v_and_b32_e32 %[" t "], %[M" k "], %[w" k "]\n\t"
+#define RZ_XOR(t, k) "v_xor_b32_e32 %[" t "], 0x40404040, %[w" k "]\n\t"
+// steps U = 1..15 of a group (byte 15 - U: dword 3 - U/4, byte 3 - U%4); step U = 0 is FIRST
+#define RZ_GROUP(P, FIRST)                                                                        \
+    P("tA", "3") P("tB", "2") FIRST RZ_STEP("tA", "2", "1", RZ_NOP) RZ_STEP("tA", "1", "2", RZ_NOP)  \
+    RZ_STEP("tA", "0", "3", RZ_NOP) RZ_STEP("tB", "3", "4", P("tA", "1"))                            \
+    RZ_STEP("tB", "2", "5", RZ_NOP) RZ_STEP("tB", "1", "6", RZ_NOP) RZ_STEP("tB", "0", "7", RZ_NOP)  \
+    RZ_STEP("tA", "3", "8", P("tB", "0")) RZ_STEP("tA", "2", "9", RZ_NOP)                            \
+    RZ_STEP("tA", "1", "10", RZ_NOP) RZ_STEP("tA", "0", "11", RZ_NOP) RZ_STEP("tB", "3", "12", RZ_NOP) \
+    RZ_STEP("tB", "2", "13", RZ_NOP) RZ_STEP("tB", "1", "14", RZ_NOP) RZ_STEP("tB", "0", "15", RZ_NOP)
+#define RZ_ENTER_X "v_xor_b32_e32 %[c0], 64, %[c0]\n\tv_xor_b32_e32 %[c1], 64, %[c1]\n\t"
+
+// the 4 masks mask(i) of dword k's bytes (byte b <-> step i = 16T + 16 - 4k - b)
+__host__ __device__ constexpr uint32_t rz_dword_masks(uint32_t T, uint32_t k) {
+    uint32_t m = 0;
+    for (uint32_t b = 0; b < 4; b++) {
+        const uint32_t i = 16u * T + 16u - 4u * k - b;
+        uint32_t mk = i;
+        for (uint32_t sh = 1; sh < 32; sh <<= 1) mk |= mk >> sh;
+        m |= (mk & 0xffu) << (8u * b);
+    }
+    return m;
+}
+
 template <uint32_t T>
-__device__ __forceinline__ void rr_walk_groups(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t nfull, uint32_t &c0,
-                                               uint32_t &c1) {
+__device__ __forceinline__ void rr_group_sdwa(const uint4 &w, uint32_t &c0, uint32_t &c1) {
+    static_assert(T < (uint32_t)RR_GROUPS, "K <= 127");
+    uint64_t mA, mB;
+    uint32_t tA, tB;
+    constexpr int ib = T >= 4u ? (int)(16u * T + 1u) - 64 : (int)(16u * T + 1u);
+#define RZ_OPS                                                                                           \
+    : [c0] "+v"(c0), [c1] "+v"(c1), [mA] "=&s"(mA), [mB] "=&s"(mB), [tA] "=&v"(tA), [tB] "=&v"(tB)    \
+    : [w0] "v"(w.x), [w1] "v"(w.y), [w2] "v"(w.z), [w3] "v"(w.w), [ib] "i"(ib),                        \
+      [M0] "i"(rz_dword_masks(T, 0)), [M1] "i"(rz_dword_masks(T, 1)), [M2] "i"(rz_dword_masks(T, 2)),  \
+      [M3] "i"(rz_dword_masks(T, 3))
+    if constexpr (T == 0u) {  // step 1 decides the final swap, not a tracker step
+        asm volatile(RZ_GROUP(RZ_AND, "") RZ_OPS);
+    } else if constexpr (T < 4u) {
+        asm volatile(RZ_GROUP(RZ_AND, RZ_STEP("tA", "3", "0", RZ_NOP)) RZ_OPS);
+    } else if constexpr (T == 4u) {
+        asm volatile(RZ_ENTER_X RZ_GROUP(RZ_XOR, RZ_STEP("tA", "3", "0", RZ_NOP)) RZ_OPS);
+    } else {
+        asm volatile(RZ_GROUP(RZ_XOR, RZ_STEP("tA", "3", "0", RZ_NOP)) RZ_OPS);
+    }
+#undef RZ_OPS
+}
+#undef RZ_CMP2
+#undef RZ_SEL2
+#undef RZ_STEP
+#undef RZ_NOP
+#undef RZ_AND
+#undef RZ_XOR
+#undef RZ_GROUP
+#undef RZ_ENTER_X
+
+template <uint32_t T>
+__device__ __forceinline__ void rr_full_groups(const uint4 (&w)[RR_GROUPS], uint32_t nfull, uint32_t &c0, uint32_t &c1) {
     if constexpr (T < (uint32_t)RR_GROUPS) {
-        const uint32_t ws[4] = {w[T].x, w[T].y, w[T].z, w[T].w};
         if (T < nfull) {
-            rr_walk_group<false, T>(ws, K, c0, c1);
-            rr_walk_groups<T + 1>(w, K, nfull, c0, c1);
-        } else if (T == nfull) {
-            rr_walk_group<true, T>(ws, K, c0, c1);
+            rr_group_sdwa<T>(w[T], c0, c1);
+            rr_full_groups<T + 1>(w, nfull, c0, c1);
         }
     }
 }
 
+template <uint32_t T>
+__device__ __forceinline__ void rr_partial_group(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t nfull, uint32_t &c0,
+                                                 uint32_t &c1) {
+    if constexpr (T < (uint32_t)RR_GROUPS) {
+        if (T == nfull) {
+            const uint32_t ws[4] = {w[T].x, w[T].y, w[T].z, w[T].w};
+            rr_walk_group<true, T>(ws, K, c0, c1);
+        } else {
+            rr_partial_group<T + 1>(w, K, nfull, c0, c1);
+        }
+    }
+}
+
+// K: the wave's longest row (uniform).  K >> 4 full groups as SDWA compares, then the group
+// holding step K (if any) step by step with its bound checked.
 __device__ __forceinline__ void rr_walk_row(const uint4 (&w)[RR_GROUPS], uint32_t K, uint32_t &c0, uint32_t &c1) {
-    rr_walk_groups<0>(w, K, K >> 4, c0, c1);  // K >> 4 groups with all 16 steps <= K
+    const uint32_t nfull = K >> 4;
+    rr_full_groups<0>(w, nfull, c0, c1);
+    if (nfull > 4u) {  // leave the XOR-64 domain of groups 4..
+        c0 ^= 64u;
+        c1 ^= 64u;
+    }
+    rr_partial_group<0>(w, K, nfull, c0, c1);
 }
 
 // Invalid steps of a lane whose chunk is shorter than the wave's longest (packed waves, below):

@@ -14,7 +14,18 @@ states by hand:
 unrolled, so the scheduler has nothing to fill the gaps with): the wait states the compiler puts
 there are its requirement for gfx950.  This test reads them from the probe's assembly and then
 walks every control-flow path of the built library's ``rng_kernel`` (both step widths) from
-each such writer to its first VALU reader, checking that no path has fewer.  A toolchain or
+each such writer to its first VALU reader, checking that no path has fewer.
+
+The resolve's full groups (``lidarslam.hip`` rr_group_sdwa) are hand-scheduled the same way:
+
+  (C) two wait states between a v_cmp writing its mask SGPR pair and the v_cndmask reading it
+      (the probe's second kernel, SDWA byte compares and selects of two dependent trackers,
+      gives the compiler's requirement);
+  (D) one between a VALU write of a VGPR and an SDWA compare reading it (the trackers and the
+      pre-masked dwords), and one between a v_cndmask and the next SDWA instruction.  The
+      compiler's own SDWA chains put an ``s_nop 0`` in those places in most but not all cases
+      (a tight pair appears in the probe too), so (D) is a conservative rule of ours rather than
+      one read off the probe.  A toolchain or
 firmware change to these hazard rules then fails here, on the CPU, instead of as a rare wrong
 draw on the GPU.
 """
@@ -166,6 +177,22 @@ def _mask_regs(x):
     return set(x.dst)
 
 
+def _cndmask_reads(x, regs):
+    return x.mnem.startswith("v_cndmask") and bool(x.src & regs)
+
+
+def _vgpr_writer(x):
+    return x.mnem.startswith("v_") and any(r.startswith("v") and r[1:].isdigit() for r in x.dst)
+
+
+def _vgpr_regs(x):
+    return {r for r in x.dst if r.startswith("v") and r[1:].isdigit()}
+
+
+def _sdwa_reads(x, regs):
+    return x.mnem.endswith("_sdwa") and bool(x.src & regs)
+
+
 @pytest.fixture(scope="module")
 def probe_waits(tmp_path_factory):
     d = tmp_path_factory.mktemp("probe")
@@ -175,8 +202,10 @@ def probe_waits(tmp_path_factory):
     ins = _parse_s(open(out).read())
     a = _min_wait(ins, _shift_writer, _shift_regs, _valu_reads)
     b = _min_wait(ins, _mask_writer, _mask_regs, _mbcnt_reads)
-    assert a is not None and b is not None, "probe: evaluation chain not found"
-    return a, b
+    c = _min_wait(ins, _mask_writer, _mask_regs, _cndmask_reads)
+    assert None not in (a, b, c), "probe: a chain not found"
+    assert any(x.mnem.endswith("_sdwa") for x in ins), "probe: no SDWA compare emitted"
+    return a, b, c
 
 
 @pytest.fixture(scope="module")
@@ -195,13 +224,14 @@ def library_code(tmp_path_factory):
 
 
 def test_probe_matches_the_documented_rules(probe_waits):
-    """The compiler's requirement is what lslam_rng_pipe.h's comment states: (A) 1, (B) 2."""
-    assert probe_waits == (1, 2)
+    """The compiler's requirement is what the sources' comments state: (A) 1, (B) 2 in
+    lslam_rng_pipe.h; (C) 2 at rr_group_sdwa."""
+    assert probe_waits == (1, 2, 2)
 
 
 @pytest.mark.parametrize("symbol", ["_Z10rng_kernelIhEv5KArgs", "_Z10rng_kernelItEv5KArgs"])
 def test_rng_kernel_asm_window_wait_states(probe_waits, library_code, symbol):
-    need_a, need_b = probe_waits
+    need_a, need_b = probe_waits[:2]
     ins = _parse_objdump(library_code, symbol)
     assert sum(x.mnem == "v_lshlrev_b64" for x in ins) >= 8, "asm table window not found"
     # (paths stop once `need` wait states have passed: a writer whose every path is padded that
@@ -210,3 +240,17 @@ def test_rng_kernel_asm_window_wait_states(probe_waits, library_code, symbol):
     b = _min_wait(ins, _mask_writer, _mask_regs, _mbcnt_reads, need=need_b)
     assert a == need_a, ("v_lshlrev_b64 -> VALU reader", a, need_a)
     assert b == need_b, ("v_cmp mask -> v_mbcnt", b, need_b)
+
+
+def test_resolve_sdwa_group_wait_states(probe_waits, library_code):
+    need_c = probe_waits[2]
+    ins = _parse_objdump(library_code, "_Z19resolve_reg8_kernel5KArgsi")
+    assert sum(x.mnem == "v_cmp_eq_u32_sdwa" for x in ins) >= 2 * 15 * 7, "SDWA groups not found"
+    c = _min_wait(ins, _mask_writer, _mask_regs, _cndmask_reads, need=need_c)
+    assert c == need_c, ("v_cmp mask -> v_cndmask", c, need_c)
+    # (D): paths stop after one wait state, so None = every pair has at least one
+    d = _min_wait(ins, _vgpr_writer, _vgpr_regs, _sdwa_reads, need=1)
+    assert d in (None, 1), ("VALU VGPR write -> SDWA read", d)
+    e = _min_wait(ins, lambda x: x.mnem.startswith("v_cndmask"), lambda x: set(),
+                  lambda x, regs: x.mnem.endswith("_sdwa"), need=1)
+    assert e in (None, 1), ("v_cndmask -> SDWA", e)

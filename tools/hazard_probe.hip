@@ -1,10 +1,12 @@
 // Hazard probe (test infrastructure, not product): the table window's fixed-point evaluation
-// (lslam_rng_pipe.h tbl_window) written in plain HIP, so that the compiler's own gfx950 hazard
-// recognizer places the wait states.  tests/test_isa_hazards.py compiles this file to assembly,
+// (lslam_rng_pipe.h tbl_window) and the resolve's tracker steps (lidarslam.hip rr_group_sdwa)
+// written in plain HIP, so that the compiler's own gfx950 hazard recognizer places the wait
+// states.  tests/test_isa_hazards.py compiles this file to assembly,
 // reads the wait states the compiler put between (a) v_lshlrev_b64 and the first VALU reading
 // its result and (b) a v_cmp writing an SGPR pair and the v_mbcnt reading it as a lane mask,
 // and checks that the hand-scheduled asm block in the built library's rng_kernel has at least
-// as many at every such pair.  The chain is fully dependent and unrolled, so the scheduler has
+// as many at every such pair; likewise (c) a v_cmp mask -> the v_cndmask reading it and (d) a
+// VALU write of a VGPR -> an SDWA instruction reading it, against resolve_reg8_kernel.  The chain is fully dependent and unrolled, so the scheduler has
 // nothing independent to fill them with: the compiler's s_nops are exactly its requirement.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,4 +23,19 @@ __global__ void hazard_probe(const uint64_t *Min, uint64_t *out) {
         R = __ballot((int32_t)hi < 0);
     }
     out[threadIdx.x] = R;
+}
+
+// (c), (d): c = (byte k of w == c) ? k + 2 : c for two trackers; the compiler emits SDWA byte
+// compares into VCC and v_cndmask_b32 selects, the trackers' chains dependent throughout.
+__global__ void hazard_probe_sel(const uint32_t *J, uint32_t *out) {
+    uint32_t c0 = J[threadIdx.x], c1 = J[64 + threadIdx.x];
+    const uint32_t w = J[128 + threadIdx.x];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t j = (w >> (8 * i)) & 0xffu;
+        c0 = (j == c0) ? (uint32_t)(i + 2) : c0;
+        c1 = (j == c1) ? (uint32_t)(i + 2) : c1;
+        asm("" : "+v"(c0), "+v"(c1));
+    }
+    out[threadIdx.x] = c0 + c1;
 }
