@@ -126,7 +126,7 @@ struct KArgs {
     int hyp_source;
     int life;
     // LDS layout (byte offsets into dynamic shared memory)
-    int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum, off_inl;
+    int off_pts, off_key, off_ring, off_draws, off_cnt, off_tied, off_tsum;
     int off_vstack, off_nstack, off_snap, off_lmk, off_vis, off_mask, off_corg, off_zobs;
     int corg_cap;
     int off_recs;       // post pass: the scan's chunk records + chunk offsets (-1: per-chunk loop)
@@ -240,12 +240,12 @@ __device__ __forceinline__ int count_pass(const double2 *P, int N, const int32_t
     return M;
 }
 
-__device__ ChunkOut chunk_finish_fit(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *inl,
+__device__ ChunkOut chunk_finish_fit(const KArgs &a, double2 *P, int N, const int32_t *draws, uint8_t *mk,
                                      int best, ChunkOut o, int lane);
 
 // The whole ransac() call for one chunk whose draws are in LDS `draws`.
-__device__ ChunkOut chunk_ransac(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *cnt,
-                                 int32_t *tied, double *tsum, int32_t *inl, double *vstack, int *nstack,
+__device__ ChunkOut chunk_ransac(const KArgs &a, double2 *P, int N, const int32_t *draws, int32_t *cnt,
+                                 int32_t *tied, double *tsum, uint8_t *mk, double *vstack, int *nstack,
                                  int32_t *cnt_out, int lane) {
     ChunkOut o;
     o.flags = 0;
@@ -304,15 +304,19 @@ __device__ ChunkOut chunk_ransac(const KArgs &a, const double2 *P, int N, const 
             }
         }
     }
-    return chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    return chunk_finish_fit(a, P, N, draws, mk, uni(best), o, lane);
 }
 
-// after selection: stop bookkeeping, inlier mask + list of the winner, refit
-__device__ ChunkOut chunk_finish_fit(const KArgs &a, const double2 *P, int N, const int32_t *draws, int32_t *inl,
+// after selection: stop bookkeeping, inlier mask of the winner, refit.  The mask pass writes the
+// LDS mask mk[0..N) and compacts the inlier points in place to P[0..nin) in data order (inlier
+// k of pass j lands at nin_j + rank <= its own index, after the pass has read its points), so the
+// refit reads them contiguously: no index list, no gathers.  P's original order is gone
+// afterwards: callers take the projections through the mask's ranks (chunk_yproj).
+__device__ ChunkOut chunk_finish_fit(const KArgs &a, double2 *P, int N, const int32_t *draws, uint8_t *mk,
                                      int best, ChunkOut o, int lane) {
     const double ecut = a.ecut;
     o.best = best;
-    __syncthreads();  // tsum (read above) and inl (written below) share LDS
+    __syncthreads();  // tsum (read above) is dead from here
     if (o.stop >= 0) {
         o.n_draws = o.stop + 2;
         o.flags |= LSLAM_EARLY_STOP;
@@ -321,20 +325,21 @@ __device__ ChunkOut chunk_finish_fit(const KArgs &a, const double2 *P, int N, co
         o.flags |= LSLAM_NO_INLIERS;
         return o;
     }
-    // inlier mask of the winner + inlier index list (data order)
+    // inlier mask of the winner; inlier points compacted to P[0..nin)
     const Model mw = model2(P[draws[2 * best]], P[draws[2 * best + 1]]);
-    int nin = 0, last = -1;
+    int nin = 0;
     for (int pb = 0; pb < N; pb += 64) {
         const int p = pb + lane;
-        const bool h = p < N && resid2(P[p < N ? p : 0], mw) < ecut;
+        const double2 q = P[p < N ? p : 0];
+        const bool h = p < N && resid2(q, mw) < ecut;
         const uint64_t bm = ballot(h);
-        if (h) inl[nin + (int)mbcnt(bm)] = p;
-        if (bm) last = pb + fls64(bm);
+        if (p < N) mk[p] = h ? 1 : 0;
+        if (h) P[nin + (int)mbcnt(bm)] = q;
         nin += popc64(bm);
     }
     __syncthreads();
     o.n_inl = nin;
-    o.last_inl = last;
+    o.last_inl = nin - 1;
     if (nin == 0) {
         o.flags |= LSLAM_NO_INLIERS;
         return o;
@@ -343,7 +348,7 @@ __device__ ChunkOut chunk_finish_fit(const KArgs &a, const double2 *P, int N, co
         o.flags |= LSLAM_EST_FAIL;
         return o;
     }
-    const Model f = (nin == 2) ? model2(P[inl[0]], P[inl[1]]) : refit_line(P, inl, nin, lane);
+    const Model f = (nin == 2) ? model2(P[0], P[1]) : refit_line(P, nin, lane);
     o.m = f;
     o.flags |= LSLAM_VALID;
     if (f.ux == 0.0) o.flags |= LSLAM_VERTICAL;
@@ -512,6 +517,15 @@ __device__ __forceinline__ void count_points_lds(const double2 *P, int N, double
     } while (0)
 #define CH_STAMP_DECL uint64_t _ch_prev = lslam_stamp();
 #define CH_STAMP_DECL_RESET _ch_prev = lslam_stamp();
+#elif defined(LSLAM_CHUNK_EXIT)
+// diagnostic build only (tools/chunkphase.sh): the wave ends after phase LSLAM_CHUNK_EXIT, so the
+// SQ instruction counters of the launch hold the phases up to it
+#define CH_STAMP_DECL_RESET
+#define CH_STAMP(k)                                           \
+    do {                                                      \
+        if ((k) == LSLAM_CHUNK_EXIT) asm volatile("s_endpgm"); \
+    } while (0)
+#define CH_STAMP_DECL
 #else
 #define CH_STAMP_DECL_RESET
 #define CH_STAMP(k) do {} while (0)
@@ -615,8 +629,8 @@ __device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecu
     return cc;
 }
 
-__device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const double2 *gP, int N, const int32_t *draws,
-                                    int32_t *cnt, int32_t *tied, double *tsum, int32_t *inl, double *vtmp,
+__device__ ChunkOut chunk_consensus(const KArgs &a, double2 *P, const double2 *gP, int N, const int32_t *draws,
+                                    int32_t *cnt, int32_t *tied, double *tsum, uint8_t *mk, double *vtmp,
                                     double *vstack, int *nstack, int32_t *cnt_out, int lane,
                                     unsigned long long *chdbg = nullptr) {
     CH_STAMP_DECL
@@ -624,7 +638,7 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
     const double ecut = a.ecut;
     const ChunkCut cc = chunk_cut(P, N, ecut, a.ecut_q, lane);
     if (N > 128 || !cc.finite || !(ecut < __builtin_inf()))
-        return chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack, cnt_out, lane);
+        return chunk_ransac(a, P, N, draws, cnt, tied, tsum, mk, vstack, nstack, cnt_out, lane);
 
     ChunkOut o;
     o.flags = 0;
@@ -739,20 +753,20 @@ __device__ ChunkOut chunk_consensus(const KArgs &a, const double2 *P, const doub
         }
     }
     CH_STAMP(3);
-    const ChunkOut of = chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    const ChunkOut of = chunk_finish_fit(a, P, N, draws, mk, uni(best), o, lane);
     CH_STAMP(4);
     return of;
 }
 
-// mask (LDS copy + global) and A8 line parameters (ransac_functions.py:25-31)
-__device__ bool finish_chunk(const KArgs &a, const ChunkOut &o, const double2 *P, const int32_t *inl, uint8_t *mk,
-                             int p0, int N, lslam_chunk_model &rec, int lane) {
+// mask (LDS copy + global) and A8 line parameters (ransac_functions.py:25-31).  A valid fit's
+// mask was written by chunk_finish_fit's pass; any other outcome has no inliers.  P holds the
+// inliers compacted (the tip is the last of them).
+__device__ bool finish_chunk(const KArgs &a, const ChunkOut &o, const double2 *P, uint8_t *mk, int p0, int N,
+                             lslam_chunk_model &rec, int lane) {
     const lslam_scan_batch &B = a.b;
     const bool valid = (o.flags & LSLAM_VALID) != 0;
-    for (int p = lane; p < N; p += 64) mk[p] = 0;
-    __syncthreads();
-    if (valid)
-        for (int k = lane; k < o.n_inl; k += 64) mk[inl[k]] = 1;
+    if (!valid)
+        for (int p = lane; p < N; p += 64) mk[p] = 0;
     __syncthreads();
     if (B.inlier_mask)
         for (int p = lane; p < N; p += 64) B.inlier_mask[p0 + p] = mk[p];
@@ -771,6 +785,20 @@ __device__ bool finish_chunk(const KArgs &a, const ChunkOut &o, const double2 *P
         rec.proj_a = av; rec.proj_b = bv;
     }
     return valid;
+}
+
+// projected points y = pa x + pb of the inliers, 0 elsewhere (ransac_functions.py:46,49,53,55),
+// with P holding the inliers compacted (chunk_finish_fit): point p's x is P[rank of p].x
+__device__ __forceinline__ void chunk_yproj(double *y, const double2 *P, const uint8_t *mk, int N, bool have_model,
+                                            double pa, double pb, int lane) {
+    int base = 0;
+    for (int pb0 = 0; pb0 < N; pb0 += 64) {
+        const int p = pb0 + lane;
+        const bool h = have_model && p < N && mk[p];
+        const uint64_t bm = ballot(h);
+        if (p < N) y[p] = h ? (pa * P[base + (int)mbcnt(bm)].x + pb) : 0.0;
+        base += popc64(bm);
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1273,7 +1301,6 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
     int32_t *cnt = (int32_t *)(smem + a.off_cnt);
     int32_t *tied = (int32_t *)(smem + a.off_tied);
     double *tsum = (double *)(smem + a.off_tsum);
-    int32_t *inl = (int32_t *)(smem + a.off_inl);
     uint8_t *mk = (uint8_t *)(smem + a.off_mask);
     double *vstack = (double *)(smem + a.off_vstack);
     int *nstack = (int *)(smem + a.off_nstack);
@@ -1438,7 +1465,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
             stage_points(B, p0, N, P, lane);
             __syncthreads();
             // ---- A4-A7
-            const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, inl, vstack, nstack,
+            const ChunkOut o = chunk_ransac(a, P, N, draws, cnt, tied, tsum, mk, vstack, nstack,
                                             B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane);
             if (use_mt && o.n_draws < D) {
                 // early stop: rewind the stream to the chunk's start, then exactly o.n_draws draws
@@ -1449,7 +1476,7 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                 __syncthreads();
                 mt_draws(mt, (uint32_t)N, (uint32_t)o.n_draws, nullptr, false, lane);
             }
-            have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
+            have_model = finish_chunk(a, o, P, mk, p0, N, rec, lane);
             if (have_model && ci < a.corg_cap && lane == 0) corg[ci] = make_double2(rec.ox, rec.oy);
         } else {
             // post pass: models and masks come from a previous ransac launch
@@ -2267,7 +2294,6 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     int32_t *cnt = (int32_t *)(smem + a.off_cnt);
     int32_t *tied = (int32_t *)(smem + a.off_tied);
     double *tsum = (double *)(smem + a.off_tsum);
-    int32_t *inl = (int32_t *)(smem + a.off_inl);
     uint8_t *mk = (uint8_t *)(smem + a.off_mask);
     double *vstack = (double *)(smem + a.off_vstack);
     int *nstack = (int *)(smem + a.off_nstack);
@@ -2329,14 +2355,11 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     __syncthreads();
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
-    const ChunkOut o = chunk_consensus(a, P, gP, N, dr, cnt, tied, tsum, inl, vtmp, vstack, nstack,
+    const ChunkOut o = chunk_consensus(a, P, gP, N, dr, cnt, tied, tsum, mk, vtmp, vstack, nstack,
                                        B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane, chdbg);
     CH_STAMP_DECL_RESET
-    const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
-    if (B.y_proj && a.write_yproj) {
-        const double pa = rec.proj_a, pb = rec.proj_b;
-        for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
-    }
+    const bool have_model = finish_chunk(a, o, P, mk, p0, N, rec, lane);
+    if (B.y_proj && a.write_yproj) chunk_yproj(B.y_proj + p0, P, mk, N, have_model, rec.proj_a, rec.proj_b, lane);
     if (lane == 0 && B.models) B.models[c] = rec;
     CH_STAMP(5);
 }
@@ -2603,7 +2626,6 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
     double2 *P = (double2 *)(smem + a.off_pts);
     int32_t *tied = (int32_t *)(smem + a.off_tied);
     double *tsum = (double *)(smem + a.off_tsum);
-    int32_t *inl = (int32_t *)(smem + a.off_inl);
     uint8_t *mk = (uint8_t *)(smem + a.off_mask);
     double *vst = (double *)(smem + a.off_vstack);
     int *nstack = (int *)(smem + a.off_nstack);
@@ -2762,13 +2784,10 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
         }
     }
     SEL_STAMP(3);
-    o = chunk_finish_fit(a, P, N, draws, inl, uni(best), o, lane);
+    o = chunk_finish_fit(a, P, N, draws, mk, uni(best), o, lane);
     SEL_STAMP(4);
-    const bool have_model = finish_chunk(a, o, P, inl, mk, p0, N, rec, lane);
-    if (B.y_proj && a.write_yproj) {
-        const double pa = rec.proj_a, pb = rec.proj_b;
-        for (int p = lane; p < N; p += 64) B.y_proj[p0 + p] = (have_model && mk[p]) ? (pa * P[p].x + pb) : 0.0;
-    }
+    const bool have_model = finish_chunk(a, o, P, mk, p0, N, rec, lane);
+    if (B.y_proj && a.write_yproj) chunk_yproj(B.y_proj + p0, P, mk, N, have_model, rec.proj_a, rec.proj_b, lane);
     if (lane == 0 && B.models) B.models[c] = rec;
     SEL_STAMP(5);
 #ifdef LSLAM_STAMPS
@@ -3369,12 +3388,11 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         k.off_pts = off; off += align16(16 * N);
         k.off_key = off; off += align16(4 * 624);
         // phase-exclusive scratch shares one region: the draw-resolution tables
-        // (draw generation), then the tie sums (selection), then the inlier list
+        // (draw generation), then the tie sums (selection)
         const int nxt_bytes = 4 * mt_nslot(N) * N;
-        const int uni_bytes = max(max(nxt_bytes, 8 * (T > 0 ? T : 1)), 4 * N);
+        const int uni_bytes = max(nxt_bytes, 8 * (T > 0 ? T : 1));
         k.off_ring = off;
         k.off_tsum = off;
-        k.off_inl = off;
         off += align16(uni_bytes);
         k.off_j1 = off;
         off += align16(4 * mt_nslot(N));
@@ -3499,9 +3517,7 @@ static int layout_chunk(KArgs &k, const lslam_scan_batch *b, int &lds) {
     k.off_draws = off; off += (k.hyp_source == LSLAM_HYP_PHILOX) ? align16(8 * (T + 1)) : 0;  // else read in place
     k.off_cnt = off; off += align16(4 * (T > 0 ? T : 1));
     k.off_tied = off; off += align16(4 * (T > 0 ? T : 1));
-    k.off_tsum = off;  // tie sums, then the inlier list
-    k.off_inl = off;
-    off += align16(max(8 * (T > 0 ? T : 1), 4 * N));
+    k.off_tsum = off; off += align16(8 * (T > 0 ? T : 1));  // tie sums
     k.off_mask = off; off += align16(N);
     k.off_vstack = off; off += (N > 128) ? align16(8 * 64 * 24) : 0;
     k.off_nstack = off; off += (N > 128) ? align16(4 * 72) : 0;
@@ -3809,7 +3825,7 @@ static int mark_calls(lslam_ctx *c) {
     return LSLAM_OK;
 }
 
-// select_kernel LDS: the chunk's points, tied trials, tie sums / inlier list, mask, sum scratch
+// select_kernel LDS: the chunk's points, tied trials, tie sums, mask, sum scratch
 static int layout_select(KArgs &k, const lslam_scan_batch *b, int &lds) {
     const int N = b->max_chunk_points > 0 ? b->max_chunk_points : 1;
     const int T = k.T > 0 ? k.T : 1;
@@ -3817,9 +3833,7 @@ static int layout_select(KArgs &k, const lslam_scan_batch *b, int &lds) {
     k.off_pts = off; off += align16(16 * N);
     k.off_tied = off; off += align16(4 * T);
     k.off_cnt = off; off += align16(4 * T);
-    k.off_tsum = off;
-    k.off_inl = off;
-    off += align16(max(8 * T, 4 * N));
+    k.off_tsum = off; off += align16(8 * T);
     k.off_mask = off; off += align16(N);
     k.off_vstack = off; off += align16(8 * 24);
     k.off_nstack = off; off += align16(4 * 72);

@@ -177,36 +177,34 @@ __device__ __forceinline__ double wave_max_d(double v) {
     return v;
 }
 
-// Final refit on the inliers inl[0..nin) (data order), nin >= 3 (fit.py:84-95).
-// The mean is numpy's axis-0 add.reduce: sequential, done by every lane.  The
-// scatter matrix for the closed-form direction is our own quantity: inlier k
-// goes to lane k % 64 (ascending k), then an xor butterfly (32, 16, ..., 1)
-// leaves the same sums in every lane.  oracle/ransac_oracle.c:scatter2
-// restates this order.
-__device__ __forceinline__ Model refit_line(const double2 *P, const int32_t *inl, int nin, int lane) {
+// Final refit on the inliers P[0..nin) (compacted in data order by chunk_finish_fit), nin >= 3
+// (fit.py:84-95).  The mean is numpy's axis-0 add.reduce: sequential, done by every lane.  The
+// scatter matrix for the closed-form direction is our own quantity: inlier k goes to lane
+// k % 64 (ascending k), then an xor butterfly (32, 16, ..., 1) leaves the same sums in every
+// lane.  oracle/ransac_oracle.c:scatter2 restates this order.
+__device__ __forceinline__ Model refit_line(const double2 *P, int nin, int lane) {
     Model f;
-    // The two sequential sums run side by side: even lanes accumulate x, odd
-    // lanes y (same additions, same order), so one v_add per inlier carries
-    // both chains and the gathers of the next inliers stay off the chain.
-    const double *Pc = (const double *)P;
-    const int comp = lane & 1;
-    double acc = Pc[2 * inl[0] + comp];
+    // The two sequential sums run side by side: even lanes accumulate x, odd lanes y (same
+    // additions, same order), so one v_add per inlier carries both chains; the inliers are
+    // contiguous, so each load is an immediate offset from one base.
+    const double *Pc = (const double *)P + (lane & 1);
+    double acc = Pc[0];
     int i = 1;
     for (; i + 8 <= nin; i += 8) {
         double v[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = Pc[2 * inl[i + j] + comp];
+        for (int j = 0; j < 8; j++) v[j] = Pc[2 * (i + j)];
 #pragma unroll
         for (int j = 0; j < 8; j++) acc += v[j];
     }
-    for (; i < nin; i++) acc += Pc[2 * inl[i] + comp];
+    for (; i < nin; i++) acc += Pc[2 * i];
     const double sx = unid(acc);                      // lane 0
     const double sy = __shfl(acc, 1);                 // lane 1
     f.ox = sx / (double)nin;
     f.oy = sy / (double)nin;
     double sxx = 0.0, sxy = 0.0, syy = 0.0;
     for (int k = lane; k < nin; k += 64) {
-        const double2 q = P[inl[k]];
+        const double2 q = P[k];
         const double cx = q.x - f.ox, cy = q.y - f.oy;
         sxx += cx * cx;
         sxy += cx * cy;

@@ -11,6 +11,7 @@
 #   profile:TAG    tools/profile_session.sh TAG (kernel trace + PMC passes)
 #   ab             tools/ab_multi.sh over $LIBS (C3 A/B of library builds, $REPS rounds)
 #   ksweep         tools/ksweep.sh (per-step time vs timed steps)
+#   chunkphase     tools/chunkphase.sh (chunk_kernel instructions per phase; variants built beforehand)
 #   rehearse2      the driver's N > 1 launch (torch.distributed.run, 2 ranks, --no-c4) with every rank
 #                  on device 0 (LSLAM_RANK_DEVICE=0)      -> gpurun_out/rehearsal_2ranks.log
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}; mkdir -p gpurun_out
@@ -46,6 +47,8 @@ for step in "$@"; do
       bash tools/ab_multi.sh || exit 1 ;;
     ksweep)
       bash tools/ksweep.sh || exit 1 ;;
+    chunkphase)
+      bash tools/chunkphase.sh || exit 1 ;;
     rehearse2)
       LSLAM_RANK_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --no-c4 --steps 20 --warmup 3 \
