@@ -28,6 +28,7 @@
 // default, which would change the reference's rounding.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include "lslam_host_math.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -121,6 +122,7 @@ struct KArgs {
     double ecut_q;  // sqrt(ecut) * 1.01 + 1 (host)
     double thr;
     double tol_a, tol_b, tol_dist;
+    double tol_dist_sq;  // largest v with RN(sqrt(v)) <= tol_dist (host: sqrt_le_bound)
     uint64_t philox_seed;
     int T;
     int hyp_source;
@@ -810,10 +812,12 @@ __device__ __forceinline__ bool is_equal(const lslam_landmark &Lk, double a, dou
     const double distA = fabs(Lk.a - a);
     const double distB = fabs(Lk.b - b);
     const double vx = Lk.end_x - px, vy = Lk.end_y - py;
-    const double dEO = cr_sqrt(__builtin_fma(vy, vy, vx * vx));
+    const double eEO = __builtin_fma(vy, vy, vx * vx);
     const double wx = Lk.pos_x - ex, wy = Lk.pos_y - ey;
-    const double dOE = cr_sqrt(__builtin_fma(wy, wy, wx * wx));
-    if (distA <= ka.tol_a && distB <= ka.tol_b) return (dEO <= ka.tol_dist || dOE <= ka.tol_dist);
+    const double eOE = __builtin_fma(wy, wy, wx * wx);
+    // landmarking.py:75-76 compare the distances sqrt(e); sqrt is correctly rounded and monotone,
+    // so RN(sqrt(e)) <= tol_dist  <=>  e <= tol_dist_sq (NaN: false either way)
+    if (distA <= ka.tol_a && distB <= ka.tol_b) return (eEO <= ka.tol_dist_sq || eOE <= ka.tol_dist_sq);
     return false;
 }
 
@@ -1099,10 +1103,10 @@ __device__ __forceinline__ bool is_equal_reg(const LmkReg &Lk, double a, double 
     const double distA = fabs(Lk.a - a);
     const double distB = fabs(Lk.b - b);
     const double vx = Lk.ex - px, vy = Lk.ey - py;
-    const double dEO = cr_sqrt(__builtin_fma(vy, vy, vx * vx));
+    const double eEO = __builtin_fma(vy, vy, vx * vx);
     const double wx = Lk.px - ex, wy = Lk.py - ey;
-    const double dOE = cr_sqrt(__builtin_fma(wy, wy, wx * wx));
-    if (distA <= ka.tol_a && distB <= ka.tol_b) return (dEO <= ka.tol_dist || dOE <= ka.tol_dist);
+    const double eOE = __builtin_fma(wy, wy, wx * wx);
+    if (distA <= ka.tol_a && distB <= ka.tol_b) return (eEO <= ka.tol_dist_sq || eOE <= ka.tol_dist_sq);
     return false;
 }
 
@@ -3375,6 +3379,7 @@ static int build_args(KArgs &k, const lslam_scan_batch *b, const lslam_ransac_pa
         k.tol_a = p->tol_a;
         k.tol_b = p->tol_b;
         k.tol_dist = p->tol_dist;
+        k.tol_dist_sq = sqrt_le_bound(p->tol_dist);
         k.philox_seed = p->philox_seed;
         k.T = p->max_trials;
         k.hyp_source = p->hyp_source;

@@ -615,3 +615,64 @@ def test_assoc_lists_stress_vs_oracle(ctx, cap):
         assert list(got["life"]) == [L["life"] for L in lst], s
         assert np.array_equal(got["a"], [L["a"] for L in lst]) and np.array_equal(got["end_y"], [L["end"][1] for L in lst])
     assert n_cap > 0  # the full-list case was exercised
+
+
+@pytest.mark.gpu
+def test_assoc_distance_at_tolerance_vs_oracle(ctx):
+    """is_equal's distance tests (landmarking.py:75-76, sqrt(e) <= TOL_DIST) at the tolerance itself:
+    the kernel compares e against the last value whose rounded square root is <= TOL_DIST
+    (lslam_host_math.h sqrt_le_bound), the oracle takes the square root.  Each scan's list holds
+    one landmark on its first fitted wall's line whose end lies k ulps around TOL_DIST from the
+    wall's origin (k = -3..2), so some match and some do not; flags, lists and y_proj must equal
+    the oracle's."""
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import LANDMARK_DTYPE, ScanPipeline
+    S = 12
+    b = synth.make_batch(list(range(700, 700 + S)), 720)
+    xy, sco, cpo = b["xy"], b["scan_chunk_off"], b["chunk_pt_off"]
+    tol = 100.0
+    lm = np.zeros((S, 8), LANDMARK_DTYPE)
+    cnt = np.zeros(S, np.int32)
+    lists_in = []
+    for s in range(S):
+        st = orc.MTState(seed=s)
+        w = None
+        for k, c in enumerate(range(sco[s], sco[s + 1])):
+            _, _, mod, _ = orc.landmark_extraction(xy[cpo[c]:cpo[c + 1]], k, [], st, cap=1)
+            if mod["flags"] & 1:
+                w = mod
+                break
+        assert w is not None
+        # the end: ox + (tol moved by k ulps), same y, so e = fl(vx * vx) with vx = fl(end_x - ox)
+        ex = w["ox"] + tol
+        for _ in range(abs(s % 6 - 3)):
+            ex = np.nextafter(ex, np.inf if s % 6 - 3 > 0 else -np.inf)
+        L = {"a": float(w["a"]), "b": float(w["b"]), "pos": (float(w["tip_x"]) + 5000.0, float(w["tip_y"]) + 5000.0),
+             "end": (float(ex), float(w["oy"])), "id": 9000 + s, "life": 40}
+        lists_in.append([L])
+        cnt[s] = 1
+        lm[s, 0] = (L["a"], L["b"], L["pos"][0], L["pos"][1], L["end"][0], L["end"][1], L["id"], L["life"])
+    id_base = (np.arange(S) * 100).astype(np.int32)
+    p = ScanPipeline(ctx, xy, sco, cpo, seeds=np.arange(S, dtype=np.uint32), landmarks=lm, lmk_count=cnt,
+                     lmk_capacity=8, id_base=id_base)
+    p.run()
+    r = p.results()
+    m = r["models"]
+    outcomes = set()
+    for s in range(S):
+        st = orc.MTState(seed=s)
+        lst = [dict(L) for L in lists_in[s]]
+        first = True
+        for k, c in enumerate(range(sco[s], sco[s + 1])):
+            p0, p1 = cpo[c], cpo[c + 1]
+            mask, yp, mod, lst = orc.landmark_extraction(xy[p0:p1], int(id_base[s]) + k, lst, st, cap=8)
+            assert np.array_equal(r["y_proj"][p0:p1], yp), (s, k)
+            for f in (64, 128, 256):
+                assert bool(m["flags"][c] & f) == bool(mod["flags"] & f), (s, k, f)
+            if first and mod["flags"] & 1:
+                outcomes.add(bool(mod["flags"] & 128))
+                first = False
+        got = r["landmarks"][s, :r["lmk_count"][s]]
+        assert list(got["id"]) == [L["id"] for L in lst], s
+        assert list(got["life"]) == [L["life"] for L in lst], s
+    assert outcomes == {True, False}  # both sides of the tolerance were exercised
