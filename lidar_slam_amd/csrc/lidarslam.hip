@@ -400,9 +400,10 @@ __device__ __forceinline__ double tie_bound_q(double S, int N, double tq) {
 typedef unsigned u32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+template <int OFF = 0>  // byte offset, the instruction's immediate
 __device__ __forceinline__ u32x16 sload_4pts(const double2 *p) {
     u32x16 v;
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(v) : "s"(p), "i"(OFF) : "memory");
     return v;
 }
 __device__ __forceinline__ u32x4 sload_pt(const double2 *p) {
@@ -441,8 +442,8 @@ __device__ __forceinline__ void count_one(double x, double y, double ux, double 
 }
 
 // one hypothesis per lane against all N points (gP: global, wave-uniform).  Groups of 4 points
-// through two SGPR buffers in turn; the loop walks a pointer (two SALU per load) and tests it
-// once per 8 points (the index form spent ~15 SALU per 4 points on 64-bit address
+// through two SGPR buffers in turn; the loop walks a pointer (one 64-bit add per 8 points, the
+// loads' offsets are immediates) and tests it once per 8 points (the index form spent ~15 SALU per 4 points on 64-bit address
 // arithmetic and two bounds tests).
 __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, double ux, double uy, double k,
                                                   cut_t r_lo, cut_t r_hi, int &lo, int &hi, double &S) {
@@ -455,13 +456,13 @@ __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, doub
         u32x16 A = sload_4pts(q), B;
         swait(A);
         while (q != qlast) {
-            B = sload_4pts(q + 4);
+            B = sload_4pts<64>(q);
             count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             swait(B);
-            A = sload_4pts(q + 8);
+            A = sload_4pts<128>(q);
             count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
             count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
@@ -469,7 +470,7 @@ __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, doub
             q += 8;
             swait(A);
         }
-        B = sload_4pts(q + 4);
+        B = sload_4pts<64>(q);
         count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
         count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
         count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
