@@ -676,3 +676,40 @@ def test_assoc_distance_at_tolerance_vs_oracle(ctx):
         assert list(got["id"]) == [L["id"] for L in lst], s
         assert list(got["life"]) == [L["life"] for L in lst], s
     assert outcomes == {True, False}  # both sides of the tolerance were exercised
+
+
+@pytest.mark.gpu
+def test_register_resolve_every_chunk_size_vs_oracle(ctx):
+    """The packed register resolve (resolve_reg8_kernel: 64 (chunk, draw) items per wave, rows of
+    different K in one wave poisoned past their K; full 16-step groups as SDWA byte compares, the
+    XOR-64 domain from step 65) over every chunk size 3..128 in one pipeline call: each scan's
+    chunks run through a different rotation of the sizes, so waves mix neighbouring sizes.  The
+    draws (draw T included: draws_out) and end states against the oracle's choice(N, 2)."""
+    from lidar_slam_amd import synth
+    from lidar_slam_amd.pipeline import ScanPipeline
+    trials = 30
+    sizes_all = list(range(3, 129))
+    S = 3
+    sizes = [sizes_all[(s * 41 + i) % len(sizes_all)] for s in range(S) for i in range(len(sizes_all))]
+    rng = np.random.default_rng(3)
+    # noisy walls: every fit has >= 3 inliers with nonzero residuals, so no chunk stops early and
+    # every chunk consumes exactly trials + 1 draws
+    xs = rng.uniform(-3000.0, 3000.0, size=sum(sizes))
+    xy = np.stack([xs, 0.3 * xs + 500.0 + rng.normal(0.0, 5.0, size=xs.size)], axis=1)
+    per = len(sizes_all)
+    sco = np.arange(0, S * per + 1, per, dtype=np.int32)
+    cpo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    seeds = np.array([21, 22, 23], np.uint32)
+    p = ScanPipeline(ctx, xy, sco, cpo, seeds=seeds, max_trials=trials, want_draws=True, want_state=True)
+    p.run()
+    r = p.results()
+    draws = r["draws"]
+    for s in range(S):
+        st = orc.MTState(seed=int(seeds[s]))
+        for k in range(per):
+            c = s * per + k
+            n = sizes[c]
+            ref = np.array([st.choice2(n) for _ in range(trials + 1)])
+            assert np.array_equal(draws[c], ref), (s, k, n)
+            assert r["models"]["n_draws"][c] == trials + 1 and not r["models"]["flags"][c] & 16, (s, k)
+        assert np.array_equal(r["mt_state"][s, :624], st.key) and r["mt_state"][s, 624] == st.pos.value, s
