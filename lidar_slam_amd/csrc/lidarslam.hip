@@ -441,6 +441,54 @@ __device__ __forceinline__ void count_one(double x, double y, double ux, double 
     asm volatile("" : "+v"(lo), "+v"(hi));  // keep one compare + add-with-carry per count
 }
 
+// Four points against the lane's hypothesis: count_one x 4 in point order (the same S chain,
+// the same counts) as one asm block.  gfx950 needs two wait states between a v_cmp writing an
+// SGPR pair and the v_addc reading it as the carry-in, and none between a v_fma_f64 and a VALU
+// reading its result (tools/hazard_probe.hip; tests/test_isa_hazards.py checks the first in the
+// code object); the compiler pads around inline asm it cannot see into, which cost the
+// point-by-point form three s_nops per point.  Here every mask is read four or more
+// instructions after its compare.  r_i lives in v[40:47] (its high dword is the FP32 key the
+// cutoffs test), the compare masks in s[80:87]; each add-with-carry writes its (unused)
+// carry-out over the mask it has just read.
+__device__ __forceinline__ void count_four(const u32x16 &A, double ux, double uy, double k, cut_t c_lo, cut_t c_hi,
+                                           int &lo, int &hi, double &S) {
+    asm volatile(
+        "v_fma_f64 v[40:41], %[y0], %[ux], %[k]\n\t"
+        "v_fma_f64 v[42:43], %[y1], %[ux], %[k]\n\t"
+        "v_fma_f64 v[44:45], %[y2], %[ux], %[k]\n\t"
+        "v_fma_f64 v[46:47], %[y3], %[ux], %[k]\n\t"
+        "v_fma_f64 v[40:41], %[x0], %[uy], -v[40:41]\n\t"
+        "v_fma_f64 v[42:43], %[x1], %[uy], -v[42:43]\n\t"
+        "v_fma_f64 v[44:45], %[x2], %[uy], -v[44:45]\n\t"
+        "v_fma_f64 v[46:47], %[x3], %[uy], -v[46:47]\n\t"
+        "v_cmp_lt_f32_e64 s[80:81], |v41|, %[cl]\n\t"
+        "v_cmp_le_f32_e64 s[82:83], |v41|, %[ch]\n\t"
+        "v_cmp_lt_f32_e64 s[84:85], |v43|, %[cl]\n\t"
+        "v_cmp_le_f32_e64 s[86:87], |v43|, %[ch]\n\t"
+        "v_fma_f64 %[S], v[40:41], v[40:41], %[S]\n\t"
+        "v_addc_co_u32_e64 %[lo], s[80:81], %[lo], 0, s[80:81]\n\t"
+        "v_addc_co_u32_e64 %[hi], s[82:83], %[hi], 0, s[82:83]\n\t"
+        "v_fma_f64 %[S], v[42:43], v[42:43], %[S]\n\t"
+        "v_cmp_lt_f32_e64 s[80:81], |v45|, %[cl]\n\t"
+        "v_cmp_le_f32_e64 s[82:83], |v45|, %[ch]\n\t"
+        "v_addc_co_u32_e64 %[lo], s[84:85], %[lo], 0, s[84:85]\n\t"
+        "v_addc_co_u32_e64 %[hi], s[86:87], %[hi], 0, s[86:87]\n\t"
+        "v_fma_f64 %[S], v[44:45], v[44:45], %[S]\n\t"
+        "v_cmp_lt_f32_e64 s[84:85], |v47|, %[cl]\n\t"
+        "v_cmp_le_f32_e64 s[86:87], |v47|, %[ch]\n\t"
+        "v_addc_co_u32_e64 %[lo], s[80:81], %[lo], 0, s[80:81]\n\t"
+        "v_addc_co_u32_e64 %[hi], s[82:83], %[hi], 0, s[82:83]\n\t"
+        "v_fma_f64 %[S], v[46:47], v[46:47], %[S]\n\t"
+        "v_addc_co_u32_e64 %[lo], s[84:85], %[lo], 0, s[84:85]\n\t"
+        "v_addc_co_u32_e64 %[hi], s[86:87], %[hi], 0, s[86:87]"
+        : [lo] "+v"(lo), [hi] "+v"(hi), [S] "+v"(S)
+        : [x0] "s"(sd(A[0], A[1])), [y0] "s"(sd(A[2], A[3])), [x1] "s"(sd(A[4], A[5])), [y1] "s"(sd(A[6], A[7])),
+          [x2] "s"(sd(A[8], A[9])), [y2] "s"(sd(A[10], A[11])), [x3] "s"(sd(A[12], A[13])),
+          [y3] "s"(sd(A[14], A[15])), [ux] "v"(ux), [uy] "v"(uy), [k] "v"(k), [cl] "v"(c_lo), [ch] "v"(c_hi)
+        : "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "s80", "s81", "s82", "s83", "s84", "s85", "s86",
+          "s87");
+}
+
 // one hypothesis per lane against all N points (gP: global, wave-uniform).  Groups of 4 points
 // through two SGPR buffers in turn; the loop walks a pointer (one 64-bit add per 8 points, the
 // loads' offsets are immediates) and tests it once per 8 points (the index form spent ~15 SALU per 4 points on 64-bit address
@@ -457,38 +505,23 @@ __device__ __forceinline__ void count_points_sgpr(const double2 *gP, int N, doub
         swait(A);
         while (q != qlast) {
             B = sload_4pts<64>(q);
-            count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_four(A, ux, uy, k, r_lo, r_hi, lo, hi, S);
             swait(B);
             A = sload_4pts<128>(q);
-            count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-            count_one(sd(B[12], B[13]), sd(B[14], B[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+            count_four(B, ux, uy, k, r_lo, r_hi, lo, hi, S);
             q += 8;
             swait(A);
         }
         B = sload_4pts<64>(q);
-        count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_four(A, ux, uy, k, r_lo, r_hi, lo, hi, S);
         swait(B);
-        count_one(sd(B[0], B[1]), sd(B[2], B[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(B[4], B[5]), sd(B[6], B[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(B[8], B[9]), sd(B[10], B[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(B[12], B[13]), sd(B[14], B[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_four(B, ux, uy, k, r_lo, r_hi, lo, hi, S);
         q += 8;
     }
     if (N & 4) {
         u32x16 A = sload_4pts(q);
         swait(A);
-        count_one(sd(A[0], A[1]), sd(A[2], A[3]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[4], A[5]), sd(A[6], A[7]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[8], A[9]), sd(A[10], A[11]), ux, uy, k, r_lo, r_hi, lo, hi, S);
-        count_one(sd(A[12], A[13]), sd(A[14], A[15]), ux, uy, k, r_lo, r_hi, lo, hi, S);
+        count_four(A, ux, uy, k, r_lo, r_hi, lo, hi, S);
         q += 4;
     }
     for (int r = N & 3; r > 0; r--, q++) {

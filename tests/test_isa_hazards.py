@@ -25,9 +25,17 @@ The resolve's full groups (``lidarslam.hip`` rr_group_sdwa) are hand-scheduled t
       pre-masked dwords), and one between a v_cndmask and the next SDWA instruction.  The
       compiler's own SDWA chains put an ``s_nop 0`` in those places in most but not all cases
       (a tight pair appears in the probe too), so (D) is a conservative rule of ours rather than
-      one read off the probe.  A toolchain or
-firmware change to these hazard rules then fails here, on the CPU, instead of as a rare wrong
-draw on the GPU.
+      one read off the probe.
+
+The consensus count loop's four-point blocks (``lidarslam.hip`` count_four) likewise:
+
+  (E) a v_fma_f64 and the first VALU reading its result: the compiler needs none (so the block
+      may chain its FMAs freely);
+  (F) two wait states between a v_cmp writing its mask SGPR pair and the v_addc reading it as
+      the carry-in (the probe's third kernel).
+
+A toolchain or firmware change to these hazard rules then fails here, on the CPU, instead of as
+a rare wrong draw or count on the GPU.
 """
 import os
 import re
@@ -181,6 +189,14 @@ def _cndmask_reads(x, regs):
     return x.mnem.startswith("v_cndmask") and bool(x.src & regs)
 
 
+def _addc_reads(x, regs):
+    return x.mnem.startswith("v_addc") and bool(x.src & regs)
+
+
+def _fma64_writer(x):
+    return x.mnem in ("v_fma_f64", "v_fmac_f64_e32")
+
+
 def _vgpr_writer(x):
     return x.mnem.startswith("v_") and any(r.startswith("v") and r[1:].isdigit() for r in x.dst)
 
@@ -203,9 +219,11 @@ def probe_waits(tmp_path_factory):
     a = _min_wait(ins, _shift_writer, _shift_regs, _valu_reads)
     b = _min_wait(ins, _mask_writer, _mask_regs, _mbcnt_reads)
     c = _min_wait(ins, _mask_writer, _mask_regs, _cndmask_reads)
-    assert None not in (a, b, c), "probe: a chain not found"
+    e = _min_wait(ins, _fma64_writer, _vgpr_regs, _valu_reads)
+    f = _min_wait(ins, _mask_writer, _mask_regs, _addc_reads)
+    assert None not in (a, b, c, e, f), "probe: a chain not found"
     assert any(x.mnem.endswith("_sdwa") for x in ins), "probe: no SDWA compare emitted"
-    return a, b, c
+    return a, b, c, e, f
 
 
 @pytest.fixture(scope="module")
@@ -225,8 +243,8 @@ def library_code(tmp_path_factory):
 
 def test_probe_matches_the_documented_rules(probe_waits):
     """The compiler's requirement is what the sources' comments state: (A) 1, (B) 2 in
-    lslam_rng_pipe.h; (C) 2 at rr_group_sdwa."""
-    assert probe_waits == (1, 2, 2)
+    lslam_rng_pipe.h; (C) 2 at rr_group_sdwa; (E) 0, (F) 2 at count_four."""
+    assert probe_waits == (1, 2, 2, 0, 2)
 
 
 @pytest.mark.parametrize("symbol", ["_Z10rng_kernelIhEv5KArgs", "_Z10rng_kernelItEv5KArgs"])
@@ -254,3 +272,15 @@ def test_resolve_sdwa_group_wait_states(probe_waits, library_code):
     e = _min_wait(ins, lambda x: x.mnem.startswith("v_cndmask"), lambda x: set(),
                   lambda x, regs: x.mnem.endswith("_sdwa"), need=1)
     assert e in (None, 1), ("v_cndmask -> SDWA", e)
+
+
+@pytest.mark.parametrize("symbol", ["_Z12chunk_kernelILi0EEv5KArgs", "_Z12chunk_kernelILi1EEv5KArgs",
+                                    "_Z12chunk_kernelILi2EEv5KArgs"])
+def test_consensus_count_block_wait_states(probe_waits, library_code, symbol):
+    need_f = probe_waits[4]
+    ins = _parse_objdump(library_code, symbol)
+    blocks = sum(x.mnem == "v_addc_co_u32_e64" and "s[80:81]" in x.ops for x in ins)
+    assert blocks >= 2 * 5, "count_four blocks not found"
+    # paths stop after need_f wait states: None or need_f = every mask -> carry-in pair has enough
+    f = _min_wait(ins, _mask_writer, _mask_regs, _addc_reads, need=need_f)
+    assert f is None or f >= need_f, ("v_cmp mask -> v_addc carry-in", f, need_f)

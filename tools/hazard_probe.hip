@@ -39,3 +39,34 @@ __global__ void hazard_probe_sel(const uint32_t *J, uint32_t *out) {
     }
     out[threadIdx.x] = c0 + c1;
 }
+
+// (e), (f): the consensus count step (lidarslam.hip count_one / count_four) as one dependent
+// chain: r = fma(x, uy, -fma(y, ux, k)), lo += |hi(r)| < c, each step's first FMA reading the
+// previous step's r.  The compiler's s_nops give (e) a v_fma_f64 -> the first VALU reading its
+// result (none needed) and (f) a v_cmp mask -> the v_addc reading it as the carry-in, against
+// chunk_kernel's hand-scheduled count_four blocks.
+__global__ void hazard_probe_count(const double *X, const float *C, int *out, double *outS) {
+    double ux = X[threadIdx.x], uy = X[64 + threadIdx.x], k = X[128 + threadIdx.x];
+    double x[4], y[4];
+    for (int i = 0; i < 4; i++) {
+        x[i] = X[192 + 64 * i + threadIdx.x];
+        y[i] = X[448 + 64 * i + threadIdx.x];
+    }
+    float c = C[threadIdx.x];
+    // every operand loaded before the chain starts (no s_waitcnt inside it)
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(ux), "+v"(uy), "+v"(k), "+v"(c));
+    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(x[i]), "+v"(y[i]));
+    int lo = 0;
+    double S = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const double r = __builtin_fma(x[i], uy, -__builtin_fma(y[i], ux, k));
+        S = __builtin_fma(r, r, S);
+        const float h = __uint_as_float((uint32_t)(__double_as_longlong(r) >> 32));
+        lo += __builtin_fabsf(h) < c ? 1 : 0;
+        asm("" : "+v"(lo), "+v"(S));
+        k = r;  // the next step's first FMA reads this one's result
+    }
+    out[threadIdx.x] = lo;
+    outS[threadIdx.x] = S;
+}
