@@ -149,16 +149,16 @@ def main():
               ", ".join("%s %.1f" % (c, per[c]) for c in CLASSES) + " = %.1f instructions." % sum(per.values()), ""]
         L += ["Per scan (%.1f in-run windows, wstamps) against the SQ counters of the profiled bench:" % nwin, "",
               "| class | in-run windows | SQ counter per scan | rest of the parser |", "|---|---|---|---|"]
-        pairs = [("VALU", ["VALU"], "SQ_INSTS_VALU"), ("SALU incl. s_nop, s_waitcnt", ["SALU", "s_nop", "s_waitcnt"], "SQ_INSTS_SALU"),
+        pairs = [("VALU", ["VALU"], "SQ_INSTS_VALU"), ("SALU (s_nop, s_waitcnt not counted)", ["SALU"], "SQ_INSTS_SALU"),
                  ("branch", ["branch"], "SQ_INSTS_BRANCH"), ("LDS", ["LDS"], "SQ_INSTS_LDS"), ("SMEM", ["SMEM"], "SQ_INSTS_SMEM")]
         for name, cs, ctr in pairs:
             a = nwin * sum(per[c] for c in cs)
             L.append("| %s | %.0f | %.0f | %.0f |" % (name, a, sq.get(ctr, 0.0), sq.get(ctr, 0.0) - a))
         L.append("| VMEM (the steps' stores) | %.0f | | |" % (nwin * per["VMEM"]))
-        L += ["", "The SALU row matches only with `s_nop` and `s_waitcnt` included: SQ_INSTS_SALU counts them. "
-              "Of the in-run window's %.1f SALU-counted instructions %.1f are `s_nop` (the hazard wait states of "
-              "tools/hazard_probe.hip, %.0f per scan) and %.1f `s_waitcnt`." % (
-                  per["SALU"] + per["s_nop"] + per["s_waitcnt"], per["s_nop"], nwin * per["s_nop"], per["s_waitcnt"])]
+        L += ["", "SQ_INSTS_SALU counts neither `s_nop` nor `s_waitcnt` (`tools/ubench_nopcount.hip`, "
+              "`profiles/r05_ubench_nopcount.txt`): the in-run window's %.1f `s_nop` (the hazard wait states of "
+              "tools/hazard_probe.hip) and %.1f `s_waitcnt`, %.0f and %.0f per scan, are issued on top of the "
+              "counters' total." % (per["s_nop"], per["s_waitcnt"], nwin * per["s_nop"], nwin * per["s_waitcnt"])]
     print("\n".join(L))
 
 
