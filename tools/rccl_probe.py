@@ -1,3 +1,5 @@
+"""One-rank RCCL communicator smoke test on device 0 (init, broadcast): does RCCL come up in
+this process beside the library's HIP context.   python tools/rccl_probe.py"""
 import os, sys, time
 sys.path.insert(0, os.getcwd())
 import numpy as np
