@@ -1854,6 +1854,12 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
         if (N < 3) continue;
         JT *Jc = J + (size_t)D * (size_t)p0;
         const int K = N - 1;
+        // the priority schedule moves at chunk starts (a block switch is ~20 times as frequent)
+        const int lvl = rp_level(rp, rp.done_steps);
+        if (lvl != rp.prio) {
+            rp.prio = lvl;
+            set_prio_level(lvl);
+        }
         const bool tbl = K <= (int)RT_KMAX && (kt0 == K || kt1 == K);
         if (tbl) {
             rp.tbl = stbl + (kt0 == K ? 0 : RT_DWORDS);

@@ -45,8 +45,8 @@ __device__ __forceinline__ void lds_flag_put(lds_flag_t *f, int v) {
 // Waves of a SIMD issue by priority, then age.  With equal priorities the
 // oldest parser of a SIMD races ahead and the youngest finishes last.
 // Parsers lower their priority as they progress (RP_PRIO_TOP in the first
-// third of the scan's steps ... RP_PRIO_TOP - 2 in the last) so the SIMD's
-// parsers advance together.  The bottom level stays above 0, the priority of
+// third of the scan's steps ... RP_PRIO_TOP - 2 in the last, checked at each
+// chunk's start) so the SIMD's parsers advance together.  The bottom level stays above 0, the priority of
 // the consumer kernels (resolve / consensus / post of the previous call) that
 // share the SIMDs: they take the issue slots the parsers' chains leave idle.
 #ifndef RP_PRIO_TOP
@@ -256,11 +256,6 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            const int lvl = rp_level(rp, rp.done_steps + g);
-            if (lvl != rp.prio) {
-                rp.prio = lvl;
-                set_prio_level(lvl);
-            }
             RP_STAMP(0);
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
@@ -567,11 +562,6 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
-            const int lvl = rp_level(rp, rp.done_steps + g);
-            if (lvl != rp.prio) {
-                rp.prio = lvl;
-                set_prio_level(lvl);
-            }
             RP_STAMP(0);
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
