@@ -144,7 +144,7 @@ struct KArgs {
     int res_g;          // resolve_kernel: LDS staging capacity (bytes)
     int32_t *draws_scr; // resolve_kernel -> chunk_kernel: [n_chunks][T+1][2] (= draws_out when given)
     uint32_t *state_scr;  // producer's end-of-scan MT state [n_scans][625]; the fix-up copies it out
-    int off_blk, off_fl, off_nxt, off_vtmp, off_stage;
+    int off_blk, off_nxt, off_vtmp, off_stage;
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int off_stbl;        // rng_kernel: [2] K claims then 2 shared reject tables, after the pipes
     const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127
@@ -1778,7 +1778,7 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
     {
         unsigned char *base = smem + (size_t)wave * a.rng_pipe_bytes;
         rp.blk = (uint32_t *)(base + a.off_blk);
-        rp.fl = (lds_flag_t *)(base + a.off_fl);
+        rp.have = 0;  // block 0 = the initial state
         rp.tbl = nullptr;
         rp.tblK = 0;
     }
@@ -1800,7 +1800,6 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
             mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
         }
     }
-    if (lane < F_NFLAGS) rp.fl[lane] = 0;
     __syncthreads();
     if (s < B.n_scans && lane == 0) {
         for (int c = B.scan_chunk_off[s]; c < B.scan_chunk_off[s + 1]; c++) {
@@ -3578,7 +3577,6 @@ static int layout_rng(KArgs &k, const lslam_scan_batch *b, int &lds) {
     if (N > 65536) return set_err(LSLAM_ERR_UNSUPPORTED, "chunks of more than 65536 points");
     int off = 0;
     k.off_blk = off; off += align16(4 * (2 * 624 + 64));  // two block slots + the head pad
-    k.off_fl = off; off += align16(4 * F_NFLAGS);
     k.rng_pipe_bytes = off;
     lds = off * RNG_PPW;
     // two K claims (16 B) + two reject tables shared by the workgroup's parsers, after the

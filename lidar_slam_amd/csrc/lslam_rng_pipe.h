@@ -28,20 +28,6 @@
 
 namespace lslam {
 
-enum { F_BLK = 0, F_NFLAGS = 8 };
-
-// flags are LDS words: keep the address space explicit, or a volatile access
-// through a generic pointer becomes a system-coherent FLAT load/store
-typedef __attribute__((address_space(3))) volatile int lds_flag_t;
-
-__device__ __forceinline__ int lds_flag_get(lds_flag_t *f) { return __builtin_amdgcn_readfirstlane(*f); }
-// v is wave-uniform: every lane stores the same word (no exec-mask juggling)
-__device__ __forceinline__ void lds_flag_put(lds_flag_t *f, int v) {
-    asm volatile("" ::: "memory");
-    *f = v;
-    asm volatile("" ::: "memory");
-}
-
 // Waves of a SIMD issue by priority, then age.  With equal priorities the
 // oldest parser of a SIMD races ahead and the youngest finishes last.
 // Parsers lower their priority as they progress (RP_PRIO_TOP in the first
@@ -118,7 +104,7 @@ __device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done);
 
 struct RngPipe {
     uint32_t *blk;         // LDS [2][624] raw MT state, block b in slot b & 1
-    lds_flag_t *fl;        // LDS [F_NFLAGS]
+    int have;              // the newest block in the pipe (wave-uniform: only its parser twists)
     uint32_t *tbl;         // LDS [RT_ROWS][RT_ST]: reject table of the current K
     uint32_t tblK;         // K of the table in tbl (0 = none)
     uint32_t total_steps;  // parser: steps of the whole scan (priority schedule)
@@ -145,17 +131,19 @@ __device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done) {
 
 // Block `need` of the pipe, before the parser reads it: twisted by the parser itself (block
 // need - 1 -> slot need & 1, which held block need - 2, already parsed; an even block also
-// refreshes the pad after slot 1).  F_BLK = the newest block in the pipe.  (A helper wave per
-// workgroup that twisted ahead was measured and dropped at r03: the parsers' chains got ~3 %
-// shorter, but the producer then held 5 instead of 4 waves per SIMD, one consumer wave fewer.)
+// refreshes the pad after slot 1).  rp.have = the newest block in the pipe, an SGPR: the
+// parser is the pipe's only writer (an LDS flag read back at every call cost an LDS round
+// trip and a readfirstlane per block).  (A helper wave per workgroup that twisted ahead was
+// measured and dropped at r03: the parsers' chains got ~3 % shorter, but the producer then
+// held 5 instead of 4 waves per SIMD, one consumer wave fewer.)
 __device__ __forceinline__ void rp_need_block(RngPipe &rp, int need, int lane) {
-    if (lds_flag_get(rp.fl + F_BLK) < need) {
+    if (rp.have < need) {
         mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N, lane);
         if ((need & 1) == 0) {
             rp.blk[2 * MT_N + lane] = rp.blk[lane];
             wave_lds_sync();
         }
-        lds_flag_put(rp.fl + F_BLK, need);
+        rp.have = need;
     }
 }
 
