@@ -562,8 +562,13 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
             uint32_t gq = g + 63u;
             const int pos_last = pos + 64 * (nrun - 1);  // the run's last window (the only CHECK one)
-            while (pos != pos_last)
+            // the unchecked windows two per loop turn (one loop test and one address step per
+            // pair: the second window's loads take the first's address plus an immediate)
+            if ((nrun - 1) & 1) tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            while (pos != pos_last) {
                 tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            }
             tbl_window<true, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
             g = gq - 63u;
             RP_STAMP(2);
