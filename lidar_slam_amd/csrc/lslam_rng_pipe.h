@@ -552,24 +552,28 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             pre_pos = -1;
             RP_STAMP(0);
         }
+        // the next block is twisted as soon as the parser enters a block (its slot held the block
+        // before this one, already parsed), so a run's last window may run across the boundary
+        // without a check: the LDS holds [block slot 0][slot 1][pad = head of slot 0], and the
+        // words after the boundary follow contiguously.  (One block per scan is twisted and never
+        // read: the one after the scan's last.)
+        rp_need_block(rp, blkno + 1, lane);
+        asm volatile("" ::: "memory");
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
         const uint32_t rem = G - g;
-        // A run of full windows short of the chunk's end, up to the block's end; the last one
-        // may run across it: the LDS holds [block slot 0][slot 1][pad = head of slot 0], so the
-        // words after the boundary follow contiguously once the helper has the next block in.
+        // A run of full windows short of the chunk's end, up to the block's end
         const int nrun = min((MT_N - pos + 63) >> 6, (int)((rem - 1u) >> 6));
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
             uint32_t gq = g + 63u;
-            const int pos_last = pos + 64 * (nrun - 1);  // the run's last window (the only CHECK one)
-            // the unchecked windows two per loop turn (one loop test and one address step per
-            // pair: the second window's loads take the first's address plus an immediate)
-            if ((nrun - 1) & 1) tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
-            while (pos != pos_last) {
+            const int pos_end = pos + 64 * nrun;
+            // two windows per loop turn (one loop test and one address step per pair: the second
+            // window's loads take the first's address plus an immediate)
+            if (nrun & 1) tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            while (pos != pos_end) {
                 tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
                 tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
             }
-            tbl_window<true, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
             g = gq - 63u;
             RP_STAMP(2);
             pre_pos = pos;
