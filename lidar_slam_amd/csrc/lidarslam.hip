@@ -1231,7 +1231,12 @@ __device__ int associate_reg(const KArgs &ka, LmkReg &e, int &L, double a, doubl
 // staged: the scan's chunk records and offsets are copied into rbuf (LDS, max_scan_chunks =
 // hist_cap records) and back; a scan with more chunks than the batch declared walks its records
 // in place (HBM) and writes y_proj chunk by chunk: the same results, one extra load per record.
-__device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool staged, int lane) {
+// STAGED (the scan's records fit the LDS area): the records are read through an LDS pointer (ds
+// loads, lgkmcnt) instead of a generic one (FLAT loads that wait on every outstanding vector memory
+// access, the y_proj prefetch included)
+template <bool staged>
+__device__ void post_assoc_reg_t(const KArgs &a, int s, unsigned char *rbuf, int lane) {
+    PS_STAMP_DECL
     const lslam_scan_batch &B = a.b;
     const int c0 = B.scan_chunk_off[s], nchunks = B.scan_chunk_off[s + 1] - c0;
     const int id0 = B.id_base ? B.id_base[s] : 0;
@@ -1255,33 +1260,61 @@ __device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool 
         e.id = 0;
         e.life = 0;
     }
+    // y_proj's inputs (inlier flags and x of up to 768 points) are loaded now, after the list, so
+    // that their latency runs under the association walk (loads complete in issue order: the
+    // walk's wait for the list does not wait for them)
+    constexpr int YPF = 12;
+    const int yq0 = B.chunk_pt_off[c0], yq1 = B.chunk_pt_off[c0 + nchunks];
+    const bool ypf = staged && B.y_proj && B.xy && yq1 - yq0 <= YPF * 64;
+    double yx[YPF];
+    asm volatile("" ::: "memory");
+    if (ypf) {
+        // unconditional loads (an index past the scan reads its first point, dropped at the use):
+        // a conditional one ends in a merge that waits for the load right there.  The inlier
+        // flags are loaded late, all at once (a byte load is widened, and so waited for, at once)
+#pragma unroll
+        for (int u = 0; u < YPF; u++) {
+            const int q0u = yq0 + u * 64 + lane;
+            yx[u] = B.xy[2 * (size_t)(q0u < yq1 ? q0u : yq0)];
+        }
+    }
     __syncthreads();
+    PS_STAMP(1);
     int32_t *walk = B.lmk_walk ? B.lmk_walk + (size_t)s * a.lmk_cap : nullptr;
     for (int ci = 0; ci < nchunks; ci++) {
-        lslam_chunk_model rec = recs[ci];
-        rec.landmark_id = id0 + ci;
-        if (rec.flags & LSLAM_VALID) {
-            double pa, pb;
+        // the record's fields read and written one by one (a copy of the whole record lived in
+        // scratch memory): landmark_id always, the association's fields for a valid line
+        lslam_chunk_model &R = recs[ci];
+        const int flags = R.flags;
+        const bool valid = (flags & LSLAM_VALID) != 0;
+        const int lid = id0 + ci;
+        int m = -1, nflags = flags;
+        double pa = 0.0, pb = 0.0;
+        if (valid) {
             bool overflow = false;
-            const int m = associate_reg(a, e, L, rec.a, rec.b, rec.ox, rec.oy, rec.tip_x, rec.tip_y,
-                                        rec.landmark_id, pa, pb, overflow, walk, lane);
-            rec.match_index = m;
-            rec.proj_a = pa;
-            rec.proj_b = pb;
-            rec.flags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
-            if (overflow) rec.flags |= LSLAM_CAPACITY;
+            m = associate_reg(a, e, L, R.a, R.b, R.ox, R.oy, R.tip_x, R.tip_y, lid, pa, pb, overflow, walk, lane);
+            nflags |= (m >= 0) ? LSLAM_MATCHED : LSLAM_NEW_LANDMARK;
+            if (overflow) nflags |= LSLAM_CAPACITY;
         }
-        __syncthreads();  // every lane has its copy of recs[ci]
-        if (lane == 0) recs[ci] = rec;
+        __syncthreads();  // every lane has read recs[ci]
+        if (lane == 0) {
+            R.landmark_id = lid;
+            if (valid) {
+                R.match_index = m;
+                R.proj_a = pa;
+                R.proj_b = pb;
+                R.flags = nflags;
+            }
+        }
         if (!staged && B.y_proj) {
             const int q0 = B.chunk_pt_off[c0 + ci], q1 = B.chunk_pt_off[c0 + ci + 1];
-            const bool have_model = (rec.flags & LSLAM_VALID) != 0;
             for (int q = q0 + lane; q < q1; q += 64) {
                 const double x = B.xy ? B.xy[2 * (size_t)q] : polar_xy(B.theta_deg[q], B.dist_mm[q]).x;
-                B.y_proj[q] = (have_model && B.inlier_mask[q]) ? (rec.proj_a * x + rec.proj_b) : 0.0;
+                B.y_proj[q] = (valid && B.inlier_mask[q]) ? (pa * x + pb) : 0.0;
             }
         }
     }
+    PS_STAMP(2);
     if (lane < L) {
         lslam_landmark g;
         g.a = e.a; g.b = e.b; g.pos_x = e.px; g.pos_y = e.py; g.end_x = e.ex; g.end_y = e.ey;
@@ -1296,7 +1329,29 @@ __device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool 
         uint4 *dst = (uint4 *)(B.models + c0);
         for (int k = lane; k < nchunks * 7; k += 64) dst[k] = src[k];
     }
+    PS_STAMP(3);
     if (!B.y_proj) return;
+    if (ypf) {
+        uint32_t ym[YPF];
+#pragma unroll
+        for (int u = 0; u < YPF; u++) {
+            const int q0u = yq0 + u * 64 + lane;
+            ym[u] = B.inlier_mask[q0u < yq1 ? q0u : yq0];
+        }
+        int ci = 0;
+#pragma unroll
+        for (int u = 0; u < YPF; u++) {
+            const int q = yq0 + u * 64 + lane;
+            if (q < yq1) {
+                while (ci + 1 < nchunks && off[ci + 1] <= q) ci++;
+                const lslam_chunk_model &r = recs[ci];
+                const bool have_model = (r.flags & LSLAM_VALID) != 0;
+                B.y_proj[q] = (have_model && ym[u]) ? (r.proj_a * yx[u] + r.proj_b) : 0.0;
+            }
+        }
+        PS_STAMP(4);
+        return;
+    }
     const int q0 = off[0], q1 = off[nchunks];
     int ci = 0;
     for (int qb = q0; qb < q1; qb += 4 * 64) {
@@ -1323,6 +1378,11 @@ __device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool 
             }
         }
     }
+    PS_STAMP(4);
+}
+__device__ void post_assoc_reg(const KArgs &a, int s, unsigned char *rbuf, bool staged, int lane) {
+    if (staged) post_assoc_reg_t<true>(a, s, rbuf, lane);
+    else post_assoc_reg_t<false>(a, s, rbuf, lane);
 }
 
 // ------------------------------------------------------------------------
@@ -1677,6 +1737,27 @@ __global__ __launch_bounds__(64) void scan_kernel(const KArgs a) {
         __syncthreads();
 #ifdef LSLAM_STAMPS
         if (!a.fixup && a.dbg && threadIdx.x == 0) {
+            a.dbg[((size_t)a.b.n_chunks + s) * 16 + 7] += lslam_stamp() - t0;
+            a.dbg[((size_t)a.b.n_chunks + s) * 16 + 8] = t0;
+        }
+#endif
+    }
+}
+// The association-only post pass with the list in registers (lmk_cap <= 64) as its own kernel:
+// inside scan_kernel it took the general scan body's register count (112 VGPRs), so only three
+// of its waves fit per SIMD beside the producer's four; alone it needs what the walk needs.
+__global__ __launch_bounds__(64) void post_reg_kernel(const KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    WAVE_CENSUS(a, WC_POST);
+    for (int s = blockIdx.x; s < a.b.n_scans; s += gridDim.x) {
+#ifdef LSLAM_STAMPS
+        const uint64_t t0 = lslam_stamp();
+#endif
+        const int nchunks = a.b.scan_chunk_off[s + 1] - a.b.scan_chunk_off[s];
+        post_assoc_reg(a, s, smem + a.off_recs, nchunks <= a.hist_cap, (int)threadIdx.x);
+        __syncthreads();
+#ifdef LSLAM_STAMPS
+        if (a.dbg && threadIdx.x == 0) {
             a.dbg[((size_t)a.b.n_chunks + s) * 16 + 7] += lslam_stamp() - t0;
             a.dbg[((size_t)a.b.n_chunks + s) * 16 + 8] = t0;
         }
@@ -3990,7 +4071,11 @@ static int launch_post(lslam_ctx *c, const KArgs &k, int lds) {
         set_max_lds(scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>);
     });
     const dim3 grid(launch_cap(c, k.b.n_scans));
-    if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
+    if (MODE == MODE_ASSOC && k.lmk_reg) {
+        static std::once_flag once_reg;
+        std::call_once(once_reg, [] { set_max_lds(post_reg_kernel); });
+        hipLaunchKernelGGL(post_reg_kernel, grid, dim3(64), lds, c->stream, k);
+    } else if (k.hyp_source == LSLAM_HYP_MT19937)  // beside the next call's producer
         hipLaunchKernelGGL((scan_kernel<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);
     else
         hipLaunchKernelGGL((scan_kernel_w4<LSLAM_HYP_EXPLICIT, MODE>), grid, dim3(64), lds, c->stream, k);

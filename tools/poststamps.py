@@ -1,5 +1,5 @@
 """Diagnostic: per-phase cycles of the post pass (association + y_proj over fitted models, s_memtime
-stamps in post_assoc_fast), C3 workload, alone and in the pipeline beside the next call's producer.
+stamps in post_assoc_reg, the register-list pass C3 takes, and post_assoc_fast), C3 workload, alone and in the pipeline beside the next call's producer.
 
 Uses the diagnostic build lidar_slam_amd/liblidarslam_stamps.so (python -m lidar_slam_amd.build
 --stamps).  Phases per scan: 1 records + offsets in, 2 association walk over the chunks, 3 records
