@@ -379,9 +379,9 @@ __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, u
     return ((uint64_t)hi << 32) | lo;
 }
 
-// One full table-mode window (64 words, short of the chunk's end).  Only the last window of a
-// run may run across the block's end (CHECK): the others skip that test, so the run loop
-// carries one backward branch per window.
+// One full table-mode window (64 words, short of the chunk's end).  The last window of a run may
+// run across the block's end: the next block is in the pipe already (parse_chunk_tbl twists it
+// when the parser enters a block), so no window tests for the crossing.
 // gq = g + 63 (steps of the chunk before this window, + 63): lane l's step is gq - s_l.
 //
 // The fixed point: three evaluations (the first at the 0.72-accepts guess s0) without a
@@ -404,17 +404,12 @@ __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, u
 // the exec restore reads EXEC as DPP data, so the block ends without a wait state (A/B at r04:
 // 0.765 vs 0.768 ms with a trailing s_nop).  The diagnostic stamp build (LSLAM_STAMPS) keeps
 // the compiler's form of the same iteration, cut into stamped segments.
-template <bool CHECK, bool KGE64, typename JT>
-__device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int blkno, int &pos, uint32_t &raw,
-                                           uint32_t &gq, uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK,
-                                           uint32_t sbase, uint32_t s0, int lane) {
-    if (CHECK && pos + 64 > MT_N) {  // crossing: wait for the next block, then reread the words
-        rp_need_block(rp, blkno + 1, lane);
-        asm volatile("" ::: "memory");
-        raw = kb[pos + lane];
-    }
+template <bool KGE64, typename JT>
+__device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int &pos, uint32_t &raw, uint32_t &gq,
+                                           uint32_t &sg, JT *__restrict__ J, uint32_t K, uint32_t mK, uint32_t sbase,
+                                           uint32_t s0, int lane) {
 #ifdef LSLAM_WSTAMPS
-    const bool wst = !CHECK;
+    const bool wst = true;
     uint64_t _w = wst ? lslam_stamp() : 0;
 #define WSTAMP(k)                                  \
     do {                                           \
@@ -431,7 +426,7 @@ __device__ __forceinline__ void tbl_window(RngPipe &rp, const uint32_t *kb, int 
 #else
 #define WSTAMP(k) do {} while (0)
 #endif
-    // next window's words (after a crossing window: discarded by the block switch)
+    // next window's words (after a window across the block's end: discarded by the block switch)
     const uint32_t nraw = kb[pos + 64 + lane];
     const uint32_t v = rt_temper_mask(raw, mK);
     WSTAMP(0);
@@ -569,10 +564,10 @@ __device__ __forceinline__ void parse_chunk_tbl(RngPipe &rp, int &blkno, int &po
             const int pos_end = pos + 64 * nrun;
             // two windows per loop turn (one loop test and one address step per pair: the second
             // window's loads take the first's address plus an immediate)
-            if (nrun & 1) tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+            if (nrun & 1) tbl_window<KGE64>(rp, kb, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
             while (pos != pos_end) {
-                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
-                tbl_window<false, KGE64>(rp, kb, blkno, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+                tbl_window<KGE64>(rp, kb, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
+                tbl_window<KGE64>(rp, kb, pos, raw, gq, sg, J, K, mK, sbase, s0, lane);
             }
             g = gq - 63u;
             RP_STAMP(2);
