@@ -253,7 +253,7 @@ def run_guarded(leg, timeout, rank, line):
     return res
 
 
-def c4_leg(args, rank, world, dist, ctx, L, segments=None):
+def c4_leg(args, rank, world, dist, ctx, L, segments=None, keep=None):
     """BASELINE configs[3] (C4): ONE host batch of ``--c4-scans`` scans split across the ranks,
     end to end.  The batch lives in one shared-memory segment of the node (the stand-in for
     the reference's mp.Queue hand-off, SLAM.py:13,18-23): rank 0 creates it, each rank fills
@@ -262,7 +262,10 @@ def c4_leg(args, rank, world, dist, ctx, L, segments=None):
     results (inlier masks, chunk records, UKF x / P, landmark counts) are gathered to rank 0's
     HBM over RCCL (lidar_slam_amd.collective: grouped send / recv on the context stream), then
     copied to rank 0's host.  Timed like the main line: barrier + sync on both sides, max over
-    ranks.  Returns the JSON object of the leg."""
+    ranks.  After the timing, one more clean step (fresh inputs and empty landmark lists) is what
+    the consistency check reads; with ``keep`` (a dict) rank 0 also leaves there the gathered
+    results of that step as the single-GPU arrays, for tests/test_gpu_c4.py.  Returns the JSON
+    object of the leg."""
     from multiprocessing import shared_memory
 
     from lidar_slam_amd import shard, synth
@@ -298,6 +301,10 @@ def c4_leg(args, rank, world, dist, ctx, L, segments=None):
             if rank != 0 and name:
                 try:
                     shm = shared_memory.SharedMemory(name=name)
+                    # attaching registers the segment with this process's resource tracker, which
+                    # would unlink it again at exit (rank 0 owns and unlinks it)
+                    from multiprocessing import resource_tracker
+                    resource_tracker.unregister(shm._name, "shared_memory")
                 except Exception as e:
                     err = e
             failed = dist.allreduce_max(0.0 if (name and err is None) else 1.0)
@@ -305,7 +312,7 @@ def c4_leg(args, rank, world, dist, ctx, L, segments=None):
                 err = RuntimeError("the C4 host batch segment could not be shared on every rank")
         if err is not None:
             raise err
-        return _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan)
+        return _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan, keep)
     finally:
         if dist is not None:
             dist.barrier()
@@ -318,7 +325,7 @@ def c4_leg(args, rank, world, dist, ctx, L, segments=None):
                 shm.unlink()
 
 
-def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
+def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan, keep=None):
     from lidar_slam_amd import collective, shard
     from lidar_slam_amd.device import DeviceArray, register_host, unregister_host
     from lidar_slam_amd.pipeline import ScanPipeline
@@ -342,7 +349,10 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
     ukf = dict(n_landmarks=L, **{k: mine["ukf_" + k] for k in ("x", "P", "u", "z", "lmk", "R_diag")})
     pipe = ScanPipeline(ctx, mine["xy"], mine["scan_chunk_off"], mine["chunk_pt_off"], seeds=mine["seeds"],
                         max_trials=args.trials, lmk_capacity=args.lmk_capacity, want_yproj=False, ukf=ukf)
-    comm = collective.Comm.from_process_group(ctx, dist)
+    if getattr(args, "c4_transport", "rccl") == "host":
+        comm = collective.HostComm(ctx, dist)
+    else:
+        comm = collective.Comm.from_process_group(ctx, dist)
     local = {"mask": pipe.mask, "models": pipe.models, "ukf_x": pipe.ukf_x, "ukf_P": pipe.ukf_P,
              "lmk_count": pipe.lmk_count}
     recv, host_out = {}, {}
@@ -383,15 +393,19 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
     for name, fn in (("h2d", h2d), ("pipeline", compute), ("gather", gather), ("d2h", d2h)):
         ts = [timed_region(fn, 1, 0, ctx.sync, barrier) for _ in range(3)]
         phases[name + "_ms"] = round(reduce_max(float(np.median(ts)), dist) * 1e3, 4)
+    # the phases above chain the landmark lists and UKF state across calls: one clean step
+    # from the shared batch's inputs is what rank 0 checks (and what a 1-GPU run would give)
+    step()
+    ctx.sync()
     res = {"workload": "C4: %d synthetic %d-pt scans in one shared host batch, %d shards of %d-%d scans; per step "
-                       "H2D + fused RANSAC/association/UKF pipeline + RCCL gather of masks, chunk records, UKF x/P "
-                       "and landmark counts to rank 0 + D2H there"
+                       "H2D + fused RANSAC/association/UKF pipeline + gather (see transport) of masks, chunk records, "
+                       "UKF x/P and landmark counts to rank 0 + D2H there"
                        % (total, args.beams, world, min(s.n_scans for s in plan), max(s.n_scans for s in plan)),
            "total_scans": total, "steps": args.c4_steps, "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
            "e2e_scans_per_s": round(total * args.c4_steps / elapsed, 1), "phases_alone": phases,
            "gathered_bytes_per_step": int(sum(v.nbytes for v in host_out.values())) if rank == 0 else None,
            "host_batch": "shared memory, %s" % ("page-locked" if pinned else "pageable"),
-           "rccl_version": collective.version(), "transport": "RCCL grouped send/recv on the lslam context stream"}
+           "rccl_version": collective.version(), "transport": comm.transport}
     if rank == 0:
         m = shard.host_view("models", host_out["models"], total)
         pop = np.add.reduceat(host_out["mask"].astype(np.int64), cpo[:-1])
@@ -399,6 +413,9 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
         res["consistent"] = bool(np.all(m["flags"] & 1) and np.array_equal(pop, m["n_inliers"]) and
                                  np.all(np.isfinite(x)) and np.array_equal(m["n_points"], np.diff(cpo)))
         res["capacity_overflows"] = capacity_overflows(m)
+        if keep is not None:
+            for k in C4_FIELDS:
+                keep[k] = shard.host_view(k, host_out[k], total).copy()
         for v in host_out.values():
             unregister_host(v)
     comm.close()
@@ -407,6 +424,56 @@ def _c4_run(args, rank, world, dist, ctx, L, shm, layout, off, sco, cpo, plan):
     if pinned:
         unregister_host(seg)
     return res
+
+
+def coupled_leg(args, ctx, b, ukf, ids, L, sync_all, barrier, dist):
+    """SURVEY §8(d)'s end-to-end step: the same batch with flags = PREDICT | UPDATE |
+    LMK_FROM_RANSAC, so landmark slot j < 8 of scan s is chunk j's fitted origin (Landmark.pos,
+    /root/reference/landmarking.py:17, ransac_functions.py:31) feeding hx (UKFMethods.py:26-34)
+    in the same call; the remaining slots keep the uniform landmarks.  The UKF then depends on
+    this call's RANSAC, so the library runs it after the consensus instead of beside it (the
+    main line's independent UKF).  z is made for that landmark set: the origins come from one
+    untimed call, the measurements are hx(pose) + N(0, R) on the host.  Timed with the main
+    line's protocol (W warmup steps, K steps between barrier + sync, max over ranks)."""
+    from lidar_slam_amd import _lib
+    from lidar_slam_amd.pipeline import ScanPipeline
+    flags = _lib.UKF_PREDICT | _lib.UKF_UPDATE | _lib.UKF_LMK_FROM_RANSAC
+    pipe = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.array(ids, np.uint32),
+                        max_trials=args.trials, lmk_capacity=args.lmk_capacity, want_yproj=True,
+                        ukf=dict(ukf, flags=flags))
+    pipe.run()
+    m = pipe.results()["models"]
+    sco = b["scan_chunk_off"]
+    nch = np.diff(sco)
+    lmk = ukf["lmk"].copy()
+    fused = 0
+    for j in range(min(L, int(nch.max()) if len(nch) else 0)):
+        s = np.nonzero(nch > j)[0]
+        c = sco[s] + j
+        ok = (m["flags"][c] & 1) != 0
+        lmk[s[ok], j, 0] = m["ox"][c[ok]]
+        lmk[s[ok], j, 1] = m["oy"][c[ok]]
+        fused += int(ok.sum())
+    poses = b["poses"]
+    rng = np.random.default_rng(515151 + int(ids[0]) if len(ids) else 515151)
+    dx = lmk[:, :, 0] - poses[:, None, 0]
+    dy = lmk[:, :, 1] - poses[:, None, 1]
+    S = len(ids)
+    d = np.sqrt(dx * dx + dy * dy) + rng.normal(0, 0.5, (S, L))
+    ph = np.arctan2(dy, dx) - poses[:, None, 2] + rng.normal(0, 0.3, (S, L))
+    ph = (ph + np.pi) % (2 * np.pi) - np.pi
+    pipe.reset_state()
+    pipe.upload_async(ukf_z=np.stack([d, ph], -1).reshape(S, 2 * L))
+    sync_all()
+    elapsed = reduce_max(timed_region(lambda: pipe.run(sync=False), args.steps, args.warmup, sync_all, barrier),
+                         dist)
+    r = pipe.results()
+    del pipe
+    return {"flags": "PREDICT|UPDATE|LMK_FROM_RANSAC", "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "scans_per_s": round(S * args.steps / elapsed * (dist.world if dist is not None else 1), 1),
+            "fused_slots_per_scan": round(fused / max(S, 1), 3), "valid_chunks": int(np.sum(r["models"]["flags"] & 1)),
+            "capacity_overflows": capacity_overflows(r["models"]),
+            "all_finite": bool(np.all(np.isfinite(r["ukf_x"])))}
 
 
 def rank_device(local_rank):
@@ -443,8 +510,12 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg at N > 1")
     ap.add_argument("--c4-scans", type=int, default=65536, help="C4: scans of the one shared batch")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-transport", default="rccl", choices=["rccl", "host"],
+                    help="C4 gather: RCCL (the product), or host TCP for a rehearsal whose ranks share one device")
     ap.add_argument("--c4-timeout", type=float, default=240.0, help="seconds before the C4 leg is abandoned")
     ap.add_argument("--no-alone", action="store_true", help="skip the producer-alone timing (profiled runs)")
+    ap.add_argument("--no-coupled", action="store_true",
+                    help="skip the coupled RANSAC->UKF step (LMK_FROM_RANSAC) of SURVEY 8(d)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -520,6 +591,11 @@ def main():
     kavg = reduce_max(kms / max(klaunch, 1), dist)
     ravg = reduce_max(rms / rl, dist) if rl else None
     cavg = reduce_max(cms / max(cl, 1), dist)
+
+    coupled = None
+    if not args.no_coupled and not args.no_ukf:
+        coupled = coupled_leg(args, ctx, b, ukf, ids, L, sync_all, barrier, dist)
+        coupled["vs_main_step"] = round(coupled["ms_per_step"] / (elapsed / args.steps * 1e3), 4)
 
     # the producer alone (no consumers beside it), for the record: lslam_hyp_mt19937 over the same batch
     alone = None
@@ -616,6 +692,7 @@ def main():
         "valid_chunks": valid,
         "capacity_overflows": overflows,
         "max_landmark_list": int(np.max(r["lmk_count"])),
+        "coupled": coupled,
     }
     if args.also_philox and world == 1:
         pipe2 = ScanPipeline(ctx, b["xy"], b["scan_chunk_off"], b["chunk_pt_off"], max_trials=args.trials,

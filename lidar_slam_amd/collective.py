@@ -131,6 +131,8 @@ def gatherv_plan(rank, world, counts, root=0):
 class Comm:
     """One rank of an RCCL communicator bound to an lslam context (its device and stream)."""
 
+    transport = "RCCL grouped send/recv on the lslam context stream"
+
     def __init__(self, ctx, world: int, rank: int, uid: bytes):
         L = load()
         self.ctx, self.world, self.rank = ctx, int(world), int(rank)
@@ -196,6 +198,49 @@ class Comm:
             pass
 
 
+class HostComm:
+    """``Comm``'s gatherv through host memory and the host group's TCP star: for a rehearsal
+    of the multi-rank launch whose ranks share ONE device (bench.py ``LSLAM_RANK_DEVICE``),
+    which RCCL refuses ("Duplicate GPU detected").  It issues the same ``gatherv_plan``: a
+    sending rank syncs its stream and ships its bytes; the root copies its own on the device
+    and uploads each peer's at its offset.  Synchronous and PCIe + TCP bound: it checks the
+    C4 leg's bookkeeping across processes, never a multi-GPU rate."""
+
+    transport = "host TCP star (rehearsal: ranks share one device)"
+
+    def __init__(self, ctx, group):
+        self.ctx, self.group = ctx, group
+        self.world = 1 if group is None else group.world
+        self.rank = 0 if group is None else group.rank
+
+    def gatherv(self, send, recv, counts, root=0):
+        import numpy as np
+        ops = gatherv_plan(self.rank, self.world, counts, root)
+        if root != 0 and self.world > 1:
+            raise ValueError("HostComm gathers to rank 0")
+        for kind, peer, off, n in ops:
+            if kind == "copy":
+                self.ctx.copy(_addr(recv, off).value, _addr(send).value, n)
+            elif kind == "send":
+                buf = np.empty(send.nbytes, np.uint8)
+                send.download(buf)  # syncs the stream: the pipeline call that wrote it is done
+                self.group.send_to_root(buf[:n].tobytes())
+            else:
+                data = np.frombuffer(self.group.recv_from(peer), np.uint8)
+                if data.size != n:
+                    raise RcclError("HostComm: rank %d sent %d bytes, expected %d" % (peer, data.size, n))
+                _lib_h2d(self.ctx, _addr(recv, off), data)
+
+    def close(self):
+        pass
+
+
+def _lib_h2d(ctx, dst, data):
+    from . import _lib
+    _lib.check(ctx._L.lslam_h2d(ctx.handle, dst, data.ctypes.data_as(C.c_void_p), data.nbytes), "lslam_h2d")
+    ctx.sync()  # data is a temporary
+
+
 def available() -> bool:
     try:
         load()
@@ -204,4 +249,4 @@ def available() -> bool:
         return False
 
 
-__all__ = ["Comm", "RcclError", "available", "gatherv_plan", "load", "unique_id", "version"]
+__all__ = ["Comm", "HostComm", "RcclError", "available", "gatherv_plan", "load", "unique_id", "version"]

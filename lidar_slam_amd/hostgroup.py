@@ -1,5 +1,6 @@
 """A minimal host-side process group for the ranks of one node: barrier, max-reduce of a
-float, broadcast of bytes.  TCP over 127.0.0.1 in a star around rank 0.
+float, broadcast of bytes, and bytes from a rank to rank 0.  TCP over 127.0.0.1 in a star
+around rank 0.
 
 bench.py's ranks need exactly these three (the barrier and max-over-ranks timing of the
 contract, and handing RCCL's 128-byte unique id and a shared-memory name around).  They
@@ -116,6 +117,18 @@ class HostGroup:
                 _send_msg(c, data)
             return data
         return _recv_msg(self.sock)
+
+    def send_to_root(self, data: bytes):
+        """A non-root rank's bytes to rank 0 (paired with ``recv_from``)."""
+        if self.rank == 0:
+            raise ValueError("send_to_root from rank 0")
+        _send_msg(self.sock, data)
+
+    def recv_from(self, rank: int) -> bytes:
+        """On rank 0: the next message ``rank`` sent with ``send_to_root``."""
+        if self.rank != 0:
+            raise ValueError("recv_from on a non-root rank")
+        return _recv_msg(self.peers[int(rank)])
 
     def close(self):
         for c in self.peers.values():

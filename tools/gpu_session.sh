@@ -14,6 +14,12 @@
 #   chunkphase     tools/chunkphase.sh (chunk_kernel instructions per phase; variants built beforehand)
 #   rehearse2      the driver's N > 1 launch (torch.distributed.run, 2 ranks, --no-c4) with every rank
 #                  on device 0 (LSLAM_RANK_DEVICE=0)      -> gpurun_out/rehearsal_2ranks.log
+#   c4one          bench.py --gpus 1 --c4: the whole 65,536-scan C4 leg at one rank -> gpurun_out/c4one.json
+#   rehearse2c4    as rehearse2 with the C4 leg ON over RCCL (expected: RCCL refuses two ranks on one
+#                  device, reported as the leg's {"error"}, main line intact) -> gpurun_out/rehearsal_2ranks_c4.log
+#   rehearse2host  as rehearse2c4 with --c4-transport host (the gather through host TCP, so shared
+#                  memory, pinning, H2D, pipeline, gather plan and D2H run in two processes)
+#                                                          -> gpurun_out/rehearsal_2ranks_host.log
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}; mkdir -p gpurun_out
 fail() { echo "step $1 failed"; tail -30 "$2"; exit 1; }
 for step in "$@"; do
@@ -54,6 +60,15 @@ for step in "$@"; do
         --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --no-c4 --steps 20 --warmup 3 \
         > gpurun_out/rehearsal_2ranks.log 2>&1 || fail $step gpurun_out/rehearsal_2ranks.log
       tail -1 gpurun_out/rehearsal_2ranks.log ;;
+    c4one)
+      timeout -k 10 400 python -u bench.py --gpus 1 --c4 --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/c4one.json 2> gpurun_out/c4one.err || fail $step gpurun_out/c4one.err
+      python3 -c "import json; d=json.load(open('gpurun_out/c4one.json')); print('C3', d['value'], d['ms_per_step'], 'coupled', d.get('coupled'), 'c4', d.get('c4'))" ;;
+    rehearse2c4|rehearse2host)
+      tr=$([ $step = rehearse2host ] && echo host || echo rccl)
+      LSLAM_RANK_DEVICE=0 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --c4 --c4-transport $tr --c4-timeout 120 \
+        --steps 20 --warmup 3 > gpurun_out/rehearsal_2ranks_$tr.log 2>&1 || fail $step gpurun_out/rehearsal_2ranks_$tr.log
+      tail -1 gpurun_out/rehearsal_2ranks_$tr.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
