@@ -4,7 +4,7 @@
 
 // The largest v with RN(sqrt(v)) <= t (IEEE sqrt, as cr_sqrt on the device): sqrt is monotone, so
 // {v >= 0 : RN(sqrt(v)) <= t} = [0, bound], and the association's distance tests
-// (landmarking.py:75-76, sqrt(e) <= TOL_DIST) become e <= bound without a square root.
+// (landmarking.py:57-72, sqrt(e) <= TOL_DIST) become e <= bound without a square root.
 // t < 0 or NaN: no v (bound -1); t = +inf: every v but NaN.
 static inline double sqrt_le_bound(double t) {
     if (std::isnan(t) || t < 0.0) return -1.0;

@@ -618,20 +618,22 @@ def test_assoc_lists_stress_vs_oracle(ctx, cap):
 
 
 @pytest.mark.gpu
-def test_assoc_distance_at_tolerance_vs_oracle(ctx):
-    """is_equal's distance tests (landmarking.py:75-76, sqrt(e) <= TOL_DIST) at the tolerance itself:
+@pytest.mark.parametrize("cap", [8, 80])
+def test_assoc_distance_at_tolerance_vs_oracle(ctx, cap):
+    """is_equal's distance tests (landmarking.py:57-72, sqrt(e) <= TOL_DIST) at the tolerance itself:
     the kernel compares e against the last value whose rounded square root is <= TOL_DIST
     (lslam_host_math.h sqrt_le_bound), the oracle takes the square root.  Each scan's list holds
     one landmark on its first fitted wall's line whose end lies k ulps around TOL_DIST from the
     wall's origin (k = -3..2), so some match and some do not; flags, lists and y_proj must equal
-    the oracle's."""
+    the oracle's.  cap = 8 runs the post pass's register list (is_equal_reg, lmk_cap <= 64),
+    cap = 80 its LDS list (is_equal)."""
     from lidar_slam_amd import synth
     from lidar_slam_amd.pipeline import LANDMARK_DTYPE, ScanPipeline
     S = 12
     b = synth.make_batch(list(range(700, 700 + S)), 720)
     xy, sco, cpo = b["xy"], b["scan_chunk_off"], b["chunk_pt_off"]
     tol = 100.0
-    lm = np.zeros((S, 8), LANDMARK_DTYPE)
+    lm = np.zeros((S, cap), LANDMARK_DTYPE)
     cnt = np.zeros(S, np.int32)
     lists_in = []
     for s in range(S):
@@ -654,7 +656,7 @@ def test_assoc_distance_at_tolerance_vs_oracle(ctx):
         lm[s, 0] = (L["a"], L["b"], L["pos"][0], L["pos"][1], L["end"][0], L["end"][1], L["id"], L["life"])
     id_base = (np.arange(S) * 100).astype(np.int32)
     p = ScanPipeline(ctx, xy, sco, cpo, seeds=np.arange(S, dtype=np.uint32), landmarks=lm, lmk_count=cnt,
-                     lmk_capacity=8, id_base=id_base)
+                     lmk_capacity=cap, id_base=id_base)
     p.run()
     r = p.results()
     m = r["models"]
@@ -665,7 +667,7 @@ def test_assoc_distance_at_tolerance_vs_oracle(ctx):
         first = True
         for k, c in enumerate(range(sco[s], sco[s + 1])):
             p0, p1 = cpo[c], cpo[c + 1]
-            mask, yp, mod, lst = orc.landmark_extraction(xy[p0:p1], int(id_base[s]) + k, lst, st, cap=8)
+            mask, yp, mod, lst = orc.landmark_extraction(xy[p0:p1], int(id_base[s]) + k, lst, st, cap=cap)
             assert np.array_equal(r["y_proj"][p0:p1], yp), (s, k)
             for f in (64, 128, 256):
                 assert bool(m["flags"][c] & f) == bool(mod["flags"] & f), (s, k, f)

@@ -1,6 +1,6 @@
 """Host-side helpers of the library (lidar_slam_amd/csrc/lslam_host_math.h), compiled with g++ on
 the CPU.  sqrt_le_bound(t) replaces the association's two square roots per landmark test
-(landmarking.py:75-76: sqrt(e) <= TOL_DIST) by e <= bound: the bound must be exactly the last
+(landmarking.py:57-72: sqrt(e) <= TOL_DIST) by e <= bound: the bound must be exactly the last
 e whose correctly rounded square root is <= t."""
 import os
 import shutil

@@ -284,3 +284,54 @@ def test_consensus_count_block_wait_states(probe_waits, library_code, symbol):
     # paths stop after need_f wait states: None or need_f = every mask -> carry-in pair has enough
     f = _min_wait(ins, _mask_writer, _mask_regs, _addc_reads, need=need_f)
     assert f is None or f >= need_f, ("v_cmp mask -> v_addc carry-in", f, need_f)
+
+
+def _lgkm_zero(x):
+    return x.mnem == "s_waitcnt" and re.search(r"lgkmcnt\(0\)", x.ops) is not None
+
+
+def _pending_sload_touches(insns):
+    """Every (s_load, instruction) pair where an instruction reads or writes the load's destination
+    SGPRs on some control-flow path before an ``s_waitcnt lgkmcnt(0)``."""
+    index = {x.addr: i for i, x in enumerate(insns)}
+    bad = []
+    for i, w in enumerate(insns):
+        if not w.mnem.startswith("s_load"):
+            continue
+        regs = w.dst
+        stack, seen = [i + 1], set()
+        while stack:
+            j = stack.pop()
+            if j >= len(insns) or j in seen:
+                continue
+            seen.add(j)
+            x = insns[j]
+            if _lgkm_zero(x):
+                continue
+            if (x.src | x.dst) & regs:
+                bad.append((hex(w.addr), w.ops, hex(x.addr), x.mnem, x.ops))
+                continue
+            if x.mnem in ("s_endpgm", "s_setpc_b64"):
+                continue
+            if x.mnem == "s_branch":
+                if x.target in index:
+                    stack.append(index[x.target])
+                continue
+            stack.append(j + 1)
+            if x.mnem.startswith("s_cbranch") and x.target in index:
+                stack.append(index[x.target])
+    return bad
+
+
+@pytest.mark.parametrize("symbol", ["_Z12chunk_kernelILi0EEv5KArgs", "_Z12chunk_kernelILi1EEv5KArgs",
+                                    "_Z12chunk_kernelILi2EEv5KArgs"])
+def test_consensus_pending_scalar_loads_untouched(library_code, symbol):
+    """count_points_sgpr keeps the next group's s_load_dwordx16 in flight while count_four runs on
+    the other buffer (its asm clobbers s[80:87]); scalar loads return out of order, so nothing may
+    read, copy or overwrite a load's destination SGPRs before the s_waitcnt lgkmcnt(0) that
+    swait() places ahead of its first use.  A compiler copy or spill of the in-flight buffer
+    would read stale points: checked on every control-flow path of the built code object."""
+    ins = _parse_objdump(library_code, symbol)
+    assert sum(x.mnem == "s_load_dwordx16" for x in ins) >= 4, "count loop's scalar loads not found"
+    bad = _pending_sload_touches(ins)
+    assert not bad, bad[:5]

@@ -6,7 +6,8 @@ Static part (CPU, from the built library): disassembles rng_kernel<u8> and, for 
 table window (the asm block's TBLA_n/TBLX_n labels), takes the loop around it -- from the loop
 header the back-edge jumps to, through the back-edge -- and sorts its instructions into
 classes.  The checked-turn loop (TBLA_n .. TBLX_n holds two turns) is counted per turn;
-everything else in the window loop once.
+everything else in the run loop once, divided by the windows one loop turn holds (two since
+r05: `windows()`).
 
 Dynamic part (GPU numbers already measured): the checked turns per window and windows per
 scan from tools/wstamps.py, the SQ_INSTS_* per scan from profile_summary.py's
@@ -88,37 +89,48 @@ def function(text, symbol):
 
 
 def windows(ins, labels):
-    """One entry per inlined window: the static counts of its loop outside the checked turns,
-    per checked turn, and whether it is a run loop (has a back-edge around the block)."""
-    res = []
+    """One entry per run loop that holds inlined table windows: the loop is the innermost
+    back-edge around a window's asm block (the checked-turn branches back to TBLA_n itself are
+    not loops of the run).  Since r05 a loop turn holds two windows (`parse_chunk_tbl`: one
+    loop test and one address step per pair), so the loop's instructions outside the windows'
+    checked-turn spans are divided by the windows it holds; each span (TBLA_n .. TBLX_n, two
+    turns) is counted per turn.  A window outside every loop (the odd window of a run with an
+    odd count, ahead of the loop) is listed by itself and not used for the per-window figure."""
     addrs = [a for a, *_ in ins]
-    for name, a_tbla in sorted(labels.items(), key=lambda kv: kv[1]):
-        if not name.startswith("TBLA"):
+    tbla = sorted((a, n) for n, a in labels.items() if n.startswith("TBLA"))
+    spans = {n: (addrs.index(a), addrs.index(labels["TBLX" + n[4:]])) for a, n in tbla}
+    loops = []  # (i_header, i_back) of back-edges that are not a checked-turn branch
+    tbla_addrs = {a for a, _ in tbla}
+    for j, (a, m, _, t) in enumerate(ins):
+        if t is not None and t < a and m.startswith(("s_cbranch", "s_branch")) and t not in tbla_addrs:
+            loops.append((addrs.index(t), j))
+    res = []
+    seen = {}
+    for a, name in tbla:
+        i_a, i_x = spans[name]
+        around = [(h, b) for h, b in loops if h <= i_a and i_x < b and b - h < 300]
+        if not around:
+            res.append({"label": name, "loop": None, "windows": 1})
             continue
-        a_tblx = labels["TBLX" + name[4:]]
-        i_a, i_x = addrs.index(a_tbla), addrs.index(a_tblx)
-        # the run loop: the first backward branch after TBLX whose target lies before TBLA
-        back = None
-        for j in range(i_x, min(i_x + 80, len(ins))):
-            t = ins[j][3]
-            if t is not None and t < a_tbla and ins[j][1].startswith("s_cbranch"):
-                back = j
-                break
-        if back is None:
-            continue
-        i_h = addrs.index(ins[back][3])
-        if a_tbla - ins[i_h][0] > 1024:  # not this window's loop
-            continue
-        fixed = {c: 0 for c in CLASSES}
+        h, b = min(around, key=lambda hb: hb[1] - hb[0])
+        seen.setdefault((h, b), []).append(name)
+    for (h, b), names in seen.items():
+        inside = {c: 0 for c in CLASSES}
         turn2 = {c: 0 for c in CLASSES}
-        for j in range(i_h, back + 1):
+        in_span = set()
+        for n in names:
+            i_a, i_x = spans[n]
+            in_span.update(range(i_a, i_x))
+        for j in range(h, b + 1):
             c = klass(ins[j][1])
-            if i_a <= j < i_x:
+            if j in in_span:
                 turn2[c] += 1
             else:
-                fixed[c] += 1
-        turn = {c: v / 2.0 for c, v in turn2.items()}
-        res.append({"label": name, "fixed": fixed, "per_turn": turn, "loop_len": back + 1 - i_h})
+                inside[c] += 1
+        nw = len(names)
+        res.append({"label": "+".join(names), "loop": (ins[h][0], ins[b][0]), "windows": nw, "loop_len": b + 1 - h,
+                    "fixed": {c: v / nw for c, v in inside.items()},
+                    "per_turn": {c: v / (2.0 * nw) for c, v in turn2.items()}})
     return res
 
 
@@ -138,12 +150,18 @@ def main():
          "from the other SALU.", "",
          "| window | loop instructions | " + " | ".join(CLASSES) + " |", "|---|---|" + "---|" * len(CLASSES)]
     for w in wins:
-        L.append("| `%s` fixed | %d | " % (w["label"], w["loop_len"]) + " | ".join("%g" % w["fixed"][c] for c in CLASSES) + " |")
+        if w["loop"] is None:
+            L.append("| `%s` (outside a loop: a run's odd first window) | | %s |" % (w["label"], " | ".join("" for _ in CLASSES)))
+            continue
+        L.append("| `%s` fixed, per window (loop %#x-%#x: %d instructions, %d windows) | %d | "
+                 % (w["label"], w["loop"][0], w["loop"][1], w["loop_len"], w["windows"], w["loop_len"]) +
+                 " | ".join("%g" % w["fixed"][c] for c in CLASSES) + " |")
         L.append("| `%s` per checked turn | | " % w["label"] + " | ".join("%g" % w["per_turn"][c] for c in CLASSES) + " |")
-    if wins and nwin:
+    looped = [w for w in wins if w["loop"] is not None]
+    if looped and nwin:
         # the dominant in-run window: C3's 100-point chunks (K = 99 >= 64: rt_wrap is one
-        # subtract-and-min, no loop), the shortest run loop
-        w = min(wins, key=lambda w: w["loop_len"])
+        # subtract-and-min, no loop), the shortest run loop per window
+        w = min(looped, key=lambda w: w["loop_len"] / w["windows"])
         per = {c: w["fixed"][c] + turns * w["per_turn"][c] for c in CLASSES}
         L += ["", "Per in-run window at %.3f checked turns (wstamps, C3), window `%s`: " % (turns, w["label"]) +
               ", ".join("%s %.1f" % (c, per[c]) for c in CLASSES) + " = %.1f instructions." % sum(per.values()), ""]
