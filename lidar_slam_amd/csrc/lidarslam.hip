@@ -148,7 +148,6 @@ struct KArgs {
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int off_stbl;        // rng_kernel: [2] K claims then 2 shared reject tables, after the pipes
     const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127
-    const uint32_t *seed_state;  // rng_kernel: seed_kernel's initial states [n_scans][624] (null: none)
     // producer epochs (one-chunk scans whose steps exceed the slot budget): this launch
     // covers draws [ep_d0, ep_d0 + ep_nd) of every chunk; ep_nd = 0: all T + 1 draws
     int ep_d0, ep_nd;
@@ -1845,31 +1844,6 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
 // RNG_PPW parser waves (one scan each) per workgroup, each twisting its own MT blocks: a
 // 4096-scan batch holds 4 waves per SIMD, and the previous call's consumers run beside it in
 // the other wave slots.
-// numpy's init_genrand (mt19937_seed, the np.random.seed(s) of every scan's stream), one lane
-// per scan.  The recurrence is sequential within a scan; the parser waves used to run it on one
-// lane each before their first twist (scalar chain + one LDS write per word: ~4.1k counted
-// instructions per scan of the producer's ~122k, SQ counters r05f).  Here 64 scans share a wave
-// (3 VALU per word for all 64), and each tile of 64 words per scan goes through LDS so a scan's
-// words leave as coalesced 256-byte rows of out[S][624].
-__global__ __launch_bounds__(64) void seed_kernel(const uint32_t *__restrict__ seeds, int S, uint32_t *__restrict__ out) {
-    __shared__ uint32_t tile[64 * 65];
-    const int lane = (int)threadIdx.x;
-    const int s0 = (int)blockIdx.x * 64;
-    const int ns = min(64, S - s0);
-    uint32_t x = (lane < ns && seeds) ? seeds[s0 + lane] : 0u;
-    for (int i0 = 0; i0 < MT_N; i0 += 64) {
-        const int n = min(64, MT_N - i0);
-        for (int i = 0; i < n; i++) {
-            tile[lane * 65 + i] = x;
-            x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i0 + i + 1);
-        }
-        wave_lds_sync();
-        if (lane < n)
-            for (int r = 0; r < ns; r++) out[(size_t)(s0 + r) * MT_N + i0 + lane] = tile[r * 65 + lane];
-        wave_lds_sync();
-    }
-}
-
 constexpr int RNG_PPW = 4;
 template <typename JT>
 __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
@@ -1900,9 +1874,6 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
     if (s < B.n_scans) {
         if (B.mt_state_in) {
             const uint32_t *src = B.mt_state_in + (size_t)s * 625;
-            for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
-        } else if (a.seed_state) {  // seeded by seed_kernel (a fresh state: pos = MT_N below)
-            const uint32_t *src = a.seed_state + (size_t)s * MT_N;
             for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
         } else {
             mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
@@ -2989,8 +2960,6 @@ struct lslam_ctx {
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h)
     uint32_t *rt_all;
-    uint32_t *seedst;     // seed_kernel -> rng_kernel: initial MT states [n_scans][624] (producer stream)
-    size_t seedst_bytes;
     size_t steps_budget;  // producer slot budget (prepare_steps)
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
@@ -3120,8 +3089,6 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->timing = false;
     c->scr = nullptr;
     c->scr_bytes = 0;
-    c->seedst = nullptr;
-    c->seedst_bytes = 0;
     c->escr = nullptr;
     c->escr_bytes = 0;
     c->cscr = nullptr;
@@ -3200,7 +3167,6 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);
     if (c->scr) (void)hipFree(c->scr);
-    if (c->seedst) (void)hipFree(c->seedst);
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
     for (int i = 0; i < NSLOTS; i++)
@@ -3839,7 +3805,6 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
 static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
     k.rt_all = c->rt_all;
-    k.seed_state = nullptr;
     int lds = 0;
     int st = layout_rng(k, &k.b, lds);
     if (st) return st;
@@ -3848,31 +3813,8 @@ static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
         set_max_lds(rng_kernel<uint8_t>);
         set_max_lds(rng_kernel<uint16_t>);
     });
-    // fresh streams (np.random.seed per scan): seeded lane-per-scan by seed_kernel on the same
-    // stream, inside the producer's timed window (LSLAM_K_RNG covers both)
-    const bool seeded = !k.b.mt_state_in && k.ep_d0 == 0 && k.b.n_scans > 0;
-    if (seeded) {
-        const size_t need = (size_t)k.b.n_scans * MT_N * 4;
-        if (c->seedst_bytes < need) {
-            HIPCHK(hipStreamSynchronize(c->stream));
-            HIPCHK(hipStreamSynchronize(c->pstream));
-            if (c->seedst) HIPCHK(hipFree(c->seedst));
-            c->seedst = nullptr;
-            c->seedst_bytes = 0;
-            hipError_t e = hipMalloc(&c->seedst, need);
-            if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (seed states)");
-            HIPCHK(e);
-            c->seedst_bytes = need;
-        }
-        k.seed_state = c->seedst;
-    }
     st = timer_begin(c, LSLAM_K_RNG, stream);
     if (st) return st;
-    if (seeded) {
-        hipLaunchKernelGGL(seed_kernel, dim3((unsigned)((k.b.n_scans + 63) / 64)), dim3(64), 0, stream, k.b.seeds,
-                           (int)k.b.n_scans, c->seedst);
-        HIPCHK(hipGetLastError());
-    }
     const dim3 grid((unsigned)((k.b.n_scans + RNG_PPW - 1) / RNG_PPW)), block(64 * RNG_PPW);
     if (k.j8) hipLaunchKernelGGL((rng_kernel<uint8_t>), grid, block, lds, stream, k);
     else hipLaunchKernelGGL((rng_kernel<uint16_t>), grid, block, lds, stream, k);
