@@ -47,29 +47,46 @@ __device__ __forceinline__ void set_prio_level(int lvl) {
     }
 }
 
-// out-of-place mt19937_gen: dst = twist(src) by one wave, three dependency phases
-__device__ __forceinline__ void mt_twist_oop(const uint32_t *src, uint32_t *dst, int lane) {
+// out-of-place mt19937_gen (numpy's, randomkit): dst = twist(src) by one wave in ten 64-word
+// chunks, i = 64 k + lane.  dst[i] = mix(src[i], src[i + 1], far) with far = src[i + 397] for
+// i < 227 and the NEW dst[i - 227] above, so chunk k reads dst only from chunks <= k - 3: four
+// groups of independent chunks ({0,1,2}, {3,4,5}, {6,7,8}, {9}), each group's loads issued
+// together after the previous group's stores.  The last word's "next" is the new dst[0] and is
+// read as src[624]: the word after the source slot, which is dst[0] itself when dst is the slot
+// after src (slot 0 -> 1), and the head pad after slot 1 when dst is slot 0 -- chunk 0 writes its
+// words there too (pad != null), which is also the pad refresh of an even block.  Every chunk
+// then runs the same code (one LDS address select in chunk 3, exec narrowed only in chunk 9);
+// the three-phase form spent 68 VALU, 30 LDS, 14 SALU and 5 branches per block and lane, most
+// of the surplus on its guarded partial iterations (SQ counters r05f).
+template <int LO, int HI>
+__device__ __forceinline__ void mt_twist_group(const uint32_t *src, uint32_t *dst, uint32_t *pad, int lane) {
+    uint32_t a[HI - LO], b[HI - LO], c[HI - LO];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = lane + 64 * k;
-        if (i < MT_N - MT_M) dst[i] = mt_mix(src[i], src[i + 1], src[i + MT_M]);
+    for (int k = LO; k < HI; k++) {
+        const int i = 64 * k + lane;
+        if (k < 9 || i < MT_N) {
+            a[k - LO] = src[i];
+            b[k - LO] = src[i + 1];
+            const uint32_t *f = (i < MT_N - MT_M) ? src + i + MT_M : dst + i - (MT_N - MT_M);
+            c[k - LO] = *f;
+        }
     }
-    wave_lds_sync();
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = (MT_N - MT_M) + lane + 64 * k;
-        if (i < 2 * (MT_N - MT_M)) dst[i] = mt_mix(src[i], src[i + 1], dst[i - (MT_N - MT_M)]);
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int i = 2 * (MT_N - MT_M) + lane + 64 * k;
-        if (i < MT_N) {
-            const uint32_t nx = (i == MT_N - 1) ? dst[0] : src[i + 1];
-            dst[i] = mt_mix(src[i], nx, dst[i - (MT_N - MT_M)]);
+    for (int k = LO; k < HI; k++) {
+        const int i = 64 * k + lane;
+        if (k < 9 || i < MT_N) {
+            const uint32_t v = mt_mix(a[k - LO], b[k - LO], c[k - LO]);
+            dst[i] = v;
+            if (k == 0 && pad) pad[lane] = v;
         }
     }
     wave_lds_sync();
+}
+__device__ __forceinline__ void mt_twist_oop(const uint32_t *src, uint32_t *dst, uint32_t *pad, int lane) {
+    mt_twist_group<0, 3>(src, dst, pad, lane);
+    mt_twist_group<3, 6>(src, dst, pad, lane);
+    mt_twist_group<6, 9>(src, dst, pad, lane);
+    mt_twist_group<9, 10>(src, dst, pad, lane);
 }
 
 // ---------------- reject tables (chunks of at most 128 points) ----------------
@@ -138,11 +155,9 @@ __device__ __forceinline__ int rp_level(const RngPipe &rp, uint32_t done) {
 // held 5 instead of 4 waves per SIMD, one consumer wave fewer.)
 __device__ __forceinline__ void rp_need_block(RngPipe &rp, int need, int lane) {
     if (rp.have < need) {
-        mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N, lane);
-        if ((need & 1) == 0) {
-            rp.blk[2 * MT_N + lane] = rp.blk[lane];
-            wave_lds_sync();
-        }
+        // an even block goes to slot 0: its head is copied to the pad after slot 1 by the twist
+        mt_twist_oop(rp.blk + ((need - 1) & 1) * MT_N, rp.blk + (need & 1) * MT_N,
+                     (need & 1) == 0 ? rp.blk + 2 * MT_N : nullptr, lane);
         rp.have = need;
     }
 }
