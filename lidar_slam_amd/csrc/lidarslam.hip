@@ -148,6 +148,7 @@ struct KArgs {
     int rng_pipe_bytes;  // rng_kernel: LDS bytes per parser pipe
     int off_stbl;        // rng_kernel: [2] K claims then 2 shared reject tables, after the pipes
     const uint32_t *rt_all;  // rng_kernel: reject tables for K = 2..127
+    const uint32_t *seed_state;  // rng_kernel: seed_kernel's initial states [n_scans][624] (null: none)
     // producer epochs (one-chunk scans whose steps exceed the slot budget): this launch
     // covers draws [ep_d0, ep_d0 + ep_nd) of every chunk; ep_nd = 0: all T + 1 draws
     int ep_d0, ep_nd;
@@ -1844,6 +1845,28 @@ static void launch_ukf_group(const KArgs &k, int n_landmarks, hipStream_t stream
 // RNG_PPW parser waves (one scan each) per workgroup, each twisting its own MT blocks: a
 // 4096-scan batch holds 4 waves per SIMD, and the previous call's consumers run beside it in
 // the other wave slots.
+// numpy's init_genrand (mt19937_seed, the np.random.seed(s) of every scan's stream), one lane
+// per scan.  The recurrence is sequential within a scan; the parser waves used to run it on one
+// lane each before their first twist (scalar chain + one LDS write per word: ~4.1k counted
+// instructions per scan of the producer's ~122k, SQ counters r05f).  Here 64 scans share a wave
+// (3 VALU per word for all 64).  No LDS: it runs beside the previous call's producer and
+// consumers (launch_seed), where a resident seed wave holding LDS could keep a producer
+// workgroup off its CU; each lane stores its own scan's row of out[S][624] (10 MB per C3 call,
+// merged in L2), and the producer's parsers read their rows coalesced.  Wave priority 2: above
+// the consumers, below the parsers, so it is done long before the next producer launches.
+__global__ __launch_bounds__(64) void seed_kernel(const uint32_t *__restrict__ seeds, int S, uint32_t *__restrict__ out) {
+    __builtin_amdgcn_s_setprio(2);
+    const int s = (int)blockIdx.x * 64 + (int)threadIdx.x;
+    if (s >= S) return;
+    uint32_t x = seeds ? seeds[s] : 0u;
+    uint32_t *row = out + (size_t)s * MT_N;
+#pragma unroll 8
+    for (int i = 0; i < MT_N; i++) {
+        row[i] = x;
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
+    }
+}
+
 constexpr int RNG_PPW = 4;
 template <typename JT>
 __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
@@ -1874,6 +1897,9 @@ __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
     if (s < B.n_scans) {
         if (B.mt_state_in) {
             const uint32_t *src = B.mt_state_in + (size_t)s * 625;
+            for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
+        } else if (a.seed_state) {  // seeded by seed_kernel (a fresh state: pos = MT_N below)
+            const uint32_t *src = a.seed_state + (size_t)s * MT_N;
             for (int i = lane; i < MT_N; i += 64) rp.blk[i] = src[i];
         } else {
             mt_seed(rp.blk, B.seeds ? B.seeds[s] : 0u, lane);
@@ -2960,6 +2986,15 @@ struct lslam_ctx {
     uint32_t timing_mask;  // kernel ids timed when timing is on (lslam_set_timing_mask)
     // reject tables of the table-mode parser, K = 2..127 (lslam_rng_pipe.h)
     uint32_t *rt_all;
+    // seed_kernel -> rng_kernel: initial MT states [n_scans][624].  [0], [1]: the pipeline's, by
+    // call parity, seeded on sstream ahead of their producers (launch_seed); [2]: producers on the
+    // ctx stream (lslam_hyp_mt19937), seeded in stream order
+    uint32_t *seedst[3];
+    size_t seedst_bytes[3];
+    hipStream_t sstream;
+    hipEvent_t ev_seeded[2];     // on sstream, after seed_kernel into seedst[i]
+    hipEvent_t ev_seed_read[2];  // on pstream, after the producer that read seedst[i]
+    int seed_next;               // the pipeline's next seed buffer
     size_t steps_budget;  // producer slot budget (prepare_steps)
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
@@ -3089,6 +3124,12 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     c->timing = false;
     c->scr = nullptr;
     c->scr_bytes = 0;
+    for (int i = 0; i < 3; i++) {
+        c->seedst[i] = nullptr;
+        c->seedst_bytes[i] = 0;
+    }
+    c->sstream = nullptr;
+    c->seed_next = 0;
     c->escr = nullptr;
     c->escr_bytes = 0;
     c->cscr = nullptr;
@@ -3137,6 +3178,12 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
         if (hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess) hi_pri = 0;
         HIPCHK(hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, hi_pri));
     }
+    HIPCHK(hipStreamCreateWithFlags(&c->sstream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(hipEventCreateWithFlags(&c->ev_seeded[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_seed_read[i], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->ev_seed_read[i], c->stream));
+    }
     for (int i = 0; i < NSLOTS; i++) HIPCHK(hipEventCreateWithFlags(&c->ev_slot_free[i], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_produced, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking));
@@ -3166,7 +3213,14 @@ int lslam_ctx_destroy(lslam_ctx *c) {
         }
     if (c->pstream) (void)hipStreamSynchronize(c->pstream);
     if (c->ustream) (void)hipStreamSynchronize(c->ustream);
+    if (c->sstream) (void)hipStreamSynchronize(c->sstream);
     if (c->scr) (void)hipFree(c->scr);
+    for (int i = 0; i < 3; i++)
+        if (c->seedst[i]) (void)hipFree(c->seedst[i]);
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_seeded[i]) (void)hipEventDestroy(c->ev_seeded[i]);
+        if (c->ev_seed_read[i]) (void)hipEventDestroy(c->ev_seed_read[i]);
+    }
     if (c->escr) (void)hipFree(c->escr);
     if (c->cscr) (void)hipFree(c->cscr);
     for (int i = 0; i < NSLOTS; i++)
@@ -3179,6 +3233,7 @@ int lslam_ctx_destroy(lslam_ctx *c) {
         if (e) (void)hipEventDestroy(e);
     if (c->pstream) (void)hipStreamDestroy(c->pstream);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
+    if (c->sstream) (void)hipStreamDestroy(c->sstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSLAM_OK;
@@ -3189,6 +3244,7 @@ int lslam_sync(lslam_ctx *c) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->pstream));
     HIPCHK(hipStreamSynchronize(c->ustream));
+    HIPCHK(hipStreamSynchronize(c->sstream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return LSLAM_OK;
 }
@@ -3802,9 +3858,58 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     return LSLAM_OK;
 }
 
+// Fresh streams (np.random.seed per scan, no mt_state_in): seed_kernel fills a seed buffer and
+// k.seed_state points the producer at it.  In the pipeline (on_side) it runs on its own stream
+// as soon as the call is enqueued -- after the input waits the producer would make (copies into
+// the seeds, a previous call writing them) and after the producer that last read its buffer
+// (two buffers by call parity) -- so it overlaps the previous call's producer, and the producer
+// only waits for its event.  Measured and dropped: seed_kernel in the producer's stream order,
+// right before rng_kernel (every producer launch 40 us later, moved onto the next resolve's
+// launch: 0.917 vs 0.715 ms per C3 step) or before its slot wait (0.786 vs 0.716 ms: the
+// producers no longer run back to back).  Returns the buffer index used (-1: none).
+static int launch_seed(lslam_ctx *c, KArgs &k, hipStream_t stream, bool on_side, bool wait_copy, bool wait_call,
+                       int &buf) {
+    k.seed_state = nullptr;
+    buf = -1;
+    if (k.b.mt_state_in || k.b.n_scans <= 0) return LSLAM_OK;
+    const int i = on_side ? c->seed_next : 2;
+    const size_t need = (size_t)k.b.n_scans * MT_N * 4;
+    if (c->seedst_bytes[i] < need) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(c->pstream));
+        HIPCHK(hipStreamSynchronize(c->sstream));
+        if (c->seedst[i]) HIPCHK(hipFree(c->seedst[i]));
+        c->seedst[i] = nullptr;
+        c->seedst_bytes[i] = 0;
+        hipError_t e = hipMalloc(&c->seedst[i], need);
+        if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (seed states)");
+        HIPCHK(e);
+        c->seedst_bytes[i] = need;
+    }
+    hipStream_t ss = stream;
+    if (on_side) {
+        ss = c->sstream;
+        HIPCHK(hipStreamWaitEvent(ss, c->ev_seed_read[i], 0));
+        if (wait_copy) HIPCHK(hipStreamWaitEvent(ss, c->ev_copy, 0));
+        if (wait_call) HIPCHK(hipStreamWaitEvent(ss, c->ev_call, 0));
+    }
+    hipLaunchKernelGGL(seed_kernel, dim3((unsigned)((k.b.n_scans + 63) / 64)), dim3(64), 0, ss, k.b.seeds,
+                       (int)k.b.n_scans, c->seedst[i]);
+    HIPCHK(hipGetLastError());
+    if (on_side) {
+        HIPCHK(hipEventRecord(c->ev_seeded[i], ss));
+        HIPCHK(hipStreamWaitEvent(stream, c->ev_seeded[i], 0));
+        c->seed_next ^= 1;
+    }
+    k.seed_state = c->seedst[i];
+    buf = on_side ? i : -1;
+    return LSLAM_OK;
+}
+
 static int launch_rng(lslam_ctx *c, const KArgs &base, hipStream_t stream) {
     KArgs k = base;
     k.rt_all = c->rt_all;
+    if (k.b.mt_state_in || k.ep_d0 != 0) k.seed_state = nullptr;  // a chained state, or a later epoch
     int lds = 0;
     int st = layout_rng(k, &k.b, lds);
     if (st) return st;
@@ -4096,6 +4201,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
     if (st) return st;
     const bool mt = k.hyp_source == LSLAM_HYP_MT19937;
     bool spec = false;
+    int seed_buf = -1;  // the seed buffer this call's producer reads (launch_seed)
     int slot = c->next_slot;
     if (mt) {
         st = prepare_steps(c, k, slot);
@@ -4147,13 +4253,14 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         HIPCHK(hipEventRecord(c->ev_ukf, c->ustream));
     }
     if (mt) {
-        // producer on its own stream: it waits for its slot's previous consumers, for input
-        // copies, and (on a hazard) for the previous call; the consumers wait for it
-        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
+        // producer on its own stream: it waits for input copies, (on a hazard) for the previous
+        // call, and for its slot's previous consumers; the consumers wait for it.  A fresh
+        // stream's seed_kernel goes between the input waits and the slot wait (launch_seed).
         // a copy into this call's MT state (e.g. a caller's upload into the previous call's
         // mt_state_out) invalidates speculating from the previous producer's end state
         const bool state_copied = copy_unknown_or_hits(c, b->mt_state_in, (size_t)b->n_scans * 625 * 4);
-        if (copy_hazard(c, b)) {
+        const bool chz = copy_hazard(c, b);
+        if (chz) {
             HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_copy, 0));
             c->n_copy_rng = 0;
             c->copy_unknown = 0;
@@ -4166,6 +4273,8 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
             c->n_out = 0;
             c->out_unknown = 0;
         }
+        if ((st = launch_seed(c, k, c->pstream, true, chz, hz == 2, seed_buf))) return st;
+        HIPCHK(hipStreamWaitEvent(c->pstream, c->ev_slot_free[slot], 0));
         // speculation (a chained stream, e.g. LandmarkMap steps): parse from the previous
         // producer's end state, which precedes this producer on pstream, instead of waiting for
         // the previous fix-up; this call's fix-up replays the scans that one replayed
@@ -4188,6 +4297,7 @@ static int run_split(lslam_ctx *c, const lslam_scan_batch *b, const lslam_ransac
         st = produce_draws(c, k, slot, c->pstream, nullptr, slot);  // slot <- the last epoch's
         k.b.mt_state_in = true_in;  // the fix-up's replays start from the true state
         if (st) return st;
+        if (seed_buf >= 0) HIPCHK(hipEventRecord(c->ev_seed_read[seed_buf], c->pstream));
     }
     // A UKF that reads nothing of this call's RANSAC runs between the fix-up and the post pass.
     // The fix-up releases this call's steps slot; the next producer starts ~40 us after that
@@ -4338,6 +4448,8 @@ int lslam_hyp_mt19937(lslam_ctx *c, const lslam_scan_batch *b, int32_t max_trial
     int last = slot;
     // on the main stream; the end state goes straight to mt_state_out
     c->resolve_beside = 0;  // alone on the ctx stream
+    int seed_buf = -1;
+    if ((st = launch_seed(c, k, c->stream, false, false, false, seed_buf))) return st;
     st = produce_draws(c, k, slot, c->stream, b->mt_state_out, last);
     if (st) return st;
     HIPCHK(hipEventRecord(c->ev_slot_free[last], c->stream));
