@@ -384,8 +384,11 @@ __device__ __forceinline__ uint32_t rt_wrap(uint32_t x, uint32_t K) {
 typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
 __device__ __forceinline__ uint64_t rt_window(const uint32_t *tbl, uint32_t v, uint32_t sg) {
     // 32-bit LDS byte address: v * 28 (v <= 127) as one u24 multiply-add onto the scalar
-    // part (table base + dword sg / 32), not a 64-bit generic-pointer multiply-add
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_u32_t *)tbl + ((sg >> 5) << 2);
+    // part (table base + dword sg / 32), not a 64-bit generic-pointer multiply-add.  The scalar
+    // part is s_lshr + s_lshl2_add (the compiler's shift, mask and add is one SALU more per window)
+    uint32_t q, base;
+    asm("s_lshr_b32 %0, %1, 5" : "=s"(q) : "s"(sg) : "scc");
+    asm("s_lshl2_add_u32 %0, %1, %2" : "=s"(base) : "s"(q), "s"((uint32_t)(uintptr_t)(lds_u32_t *)tbl) : "scc");
     lds_u32_t *row = (lds_u32_t *)(uintptr_t)(__umul24(v, RT_ST * 4u) + base);
     const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
     const uint32_t r = sg & 31u;
