@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:?tag}; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="bench.py --no-cpu-baseline --no-alone $*"
+B="bench.py --no-cpu-baseline --no-alone --no-coupled $*"
 run() { local t=$1; shift; echo "== $*" >&2; timeout -k 10 "$t" "$@"; local rc=$?; echo "rc=$rc" >&2; return $rc; }
 run 240 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $B --steps 10 --warmup 2 > $OUT/kt.log 2>&1 || exit 1
 run 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- python3 $B --steps 3 --warmup 1 > $OUT/fetch.log 2>&1 || exit 1
