@@ -650,7 +650,9 @@ def main():
                 "kernel": "rng_kernel (MT19937 parse, lslam_rng_pipe.h)", "kernel_ms": round(ravg, 4),
                 "kernel_alone_ms": round(alone, 4) if alone else None,
                 "ops_per_launch": round(ops), "ops_def": "%d per MT word (expected words from random_interval's "
-                "acceptance) + %d per Fisher-Yates step" % (OPS_PER_WORD, OPS_PER_STEP)}
+                "acceptance) + %d per Fisher-Yates step" % (OPS_PER_WORD, OPS_PER_STEP),
+                "not_in_kernel_ms": "seed_kernel (numpy init_genrand of every scan, lane per scan, on its own "
+                                    "stream beside the previous call; ~20 us per call in rocprof, DESIGN.md §4.1)"}
     else:
         roof = {"bound": "fp64-valu", "achieved": round(cons_tf, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "traffic": traffic_of("chunk_kernel"),
