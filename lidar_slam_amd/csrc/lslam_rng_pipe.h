@@ -268,18 +268,22 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
         const int nrun = FAST ? min((MT_N - pos) >> 6, (int)((rem - 1u) >> 6)) : 0;
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
+            // software-pipelined temper: window r+1's words are tempered beside window r's fixed
+            // point (this path is latency-bound: C5's one-chunk scans give 4 parsers per SIMD and
+            // little else to issue, ~680 cycles per window alone, stamps r06)
+            uint32_t w = rt_temper_mask(raw, 0xffffffffu);
             for (int r = 0; r < nrun; r++) {
                 // next window's words: past the block's end this reads the rest of the pipe's LDS
                 // (the other block, the flags, the next pipe) or out-of-range zeros; never used
                 const uint32_t nraw = kb[pos + 64 + lane];
                 RP_STAMP(3);
                 const uint32_t b1 = K - 1u - sg;
-                const uint32_t w = rt_temper_mask(raw, 0xffffffffu);
                 const uint32_t base0 = b1 - (uint32_t)lane;
                 uint32_t d = b1 - guess;
                 uint32_t i = fy_index(d, K);
                 uint32_t jv = fy_j(w, i);
                 uint64_t R = ballot(jv > i), Rp;
+                const uint32_t wn = rt_temper_mask(nraw, 0xffffffffu);
                 int it = 1;
                 do {
                     Rp = R;
@@ -302,6 +306,7 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
                 sg += na;
                 if (sg >= K) sg -= K;
                 raw = nraw;
+                w = wn;
             }
             pre_pos = pos;
             pre_raw = raw;

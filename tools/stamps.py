@@ -2,7 +2,8 @@
 
 Uses the separate diagnostic build lidar_slam_amd/liblidarslam_stamps.so
 (python -m lidar_slam_amd.build --stamps); the product library has no stamps.  Read the
-SHARES, not the absolute time (stamps serialise the wave)."""
+SHARES, not the absolute time (stamps serialise the wave).
+    python tools/stamps.py [scans] [c5]   (c5: 4096-point one-chunk scans, 2048 trials: mask mode)"""
 import ctypes as C
 import json
 import os
@@ -22,12 +23,18 @@ from lidar_slam_amd import pipeline as pl  # noqa: E402
 from lidar_slam_amd.device import Context  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+C5 = len(sys.argv) > 2 and sys.argv[2] == "c5"  # C5: one 4096-point chunk per scan, 2048 trials (mask mode, epochs)
 ctx = Context(0)
-b, _ = make_workload(list(range(S)), 720, 20)
+if C5:
+    sco = np.arange(S + 1, dtype=np.int32)
+    cpo = (np.arange(S + 1) * 4096).astype(np.int32)
+else:
+    b, _ = make_workload(list(range(S)), 720, 20)
+    sco, cpo = b["scan_chunk_off"], b["chunk_pt_off"]
 dbg = ctx.empty((S, 16), np.uint64)
 dbg.fill_zero()
 L.lslam_debug_set_stamps(dbg.ptr)
-pl.hyp_mt19937(ctx, b["scan_chunk_off"], b["chunk_pt_off"], seeds=np.arange(S))
+pl.hyp_mt19937(ctx, sco, cpo, seeds=np.arange(S), max_trials=2048 if C5 else 100)
 acc = dbg.download().astype(np.float64)
 names = ["block_wait", "unused", "fixed_point", "rest", "start_time", "windows", "fp_iterations",
          "parser_total"]
