@@ -2394,14 +2394,25 @@ __global__ __launch_bounds__(64) void resolve_walk_kernel(const KArgs a) {
                 m1 = ballot(jv == c1) & ((~0ull << l) << 1);
             }
         };
-        // RW windows at a time, their loads issued together; in the last group the lanes past K
-        // read step K (in range) and never match
-        for (uint32_t ib = 2; ib <= K; ib += 64u * RW) {
-            uint32_t raw[RW];
+        // Groups of RW windows, their loads issued together; in the last group the lanes past K
+        // read step K (in range) and never match.  Double-buffered: group g + 1's loads are in
+        // flight while group g is walked (beside the next epoch's parsers a wave otherwise
+        // waited out each group's load latency with nothing to issue).
+        auto load_group = [&](uint32_t ib, uint32_t (&raw)[RW]) {
             if (ib + 64u * RW - 1u <= K) {
                 const JT *q = Jd + (K - ib - (uint32_t)lane);
 #pragma unroll
                 for (int u = 0; u < RW; u++) raw[u] = (uint32_t)q[-64 * u];
+            } else {
+#pragma unroll
+                for (int u = 0; u < RW; u++) {
+                    const uint32_t i = ib + 64u * (uint32_t)u + (uint32_t)lane;
+                    raw[u] = (uint32_t)Jd[K - (i <= K ? i : K)];
+                }
+            }
+        };
+        auto walk_group = [&](uint32_t ib, const uint32_t (&raw)[RW]) {
+            if (ib + 64u * RW - 1u <= K) {
 #pragma unroll
                 for (int u = 0; u < RW; u++) {
                     const uint32_t i = ib + 64u * (uint32_t)u + (uint32_t)lane;
@@ -2410,16 +2421,21 @@ __global__ __launch_bounds__(64) void resolve_walk_kernel(const KArgs a) {
             } else {
 #pragma unroll
                 for (int u = 0; u < RW; u++) {
-                    const uint32_t i = ib + 64u * (uint32_t)u + (uint32_t)lane;
-                    raw[u] = (uint32_t)Jd[K - (i <= K ? i : K)];
-                }
-#pragma unroll
-                for (int u = 0; u < RW; u++) {
                     const uint32_t i0 = ib + 64u * (uint32_t)u, i = i0 + (uint32_t)lane;
                     if (i0 > K) break;
                     track(i <= K ? (raw[u] & step_mask(i)) : 0xffffffffu, i0);
                 }
             }
+        };
+        uint32_t rawA[RW], rawB[RW];
+        if (2u <= K) load_group(2u, rawA);
+        for (uint32_t ib = 2; ib <= K; ib += 128u * RW) {
+            const uint32_t ib2 = ib + 64u * RW;
+            if (ib2 <= K) load_group(ib2, rawB);
+            walk_group(ib, rawA);
+            if (ib2 > K) break;
+            if (ib2 + 64u * RW <= K) load_group(ib2 + 64u * RW, rawA);
+            walk_group(ib2, rawB);
         }
         if (lane == 0) {
             const uint32_t j1 = (uint32_t)Jd[K - 1u] & 1u;
@@ -3819,10 +3835,13 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     k.res_g = lds;  // staging capacity in bytes
     if (lds == 0) {  // steps streamed from HBM, waves over (chunk, draw)
         const int64_t items = (int64_t)k.b.n_chunks * De;
-        // beside the next epoch's producer (produce_draws): two waves per SIMD, so its parsers
-        // keep their residency (three per SIMD displaced them: C5 107 vs 78 ms per call).
-        // (Measured and dropped: LDS tiles of [64 draws][128 steps], 1.0 vs 0.43 ms per epoch.)
-        const int64_t cap = k.ep_count > 1 ? 8 * (int64_t)c->n_cus : (1 << 20);
+        // beside the next epoch's producer (produce_draws): three waves per SIMD beside its four
+        // parsers (r06, with the double-buffered walk: C5 65.7-66.1 vs 68.9-69.3 ms per call at
+        // two, 66.0-66.3 at four; the epoch loop is max(producer, resolve beside it), and at two
+        // the resolve was the longer).  (At r02, with five producer waves per SIMD, three
+        // displaced parser workgroups: 107 vs 78 ms.  Measured and dropped: LDS tiles of
+        // [64 draws][128 steps], 1.0 vs 0.43 ms per epoch.)
+        const int64_t cap = k.ep_count > 1 ? 12 * (int64_t)c->n_cus : (1 << 20);
         const dim3 grid(launch_cap(c, items > cap ? cap : items)), block(64);
         if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, rs, k);
         else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, rs, k);

@@ -259,6 +259,14 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
             asm volatile("" ::: "memory");
             pos -= MT_N;  // > 0 after a window that ran across the block boundary (table mode)
             pre_pos = -1;
+            // the priority schedule at block switches too: a one-chunk scan (C5) has no other
+            // chunk start, and without it a SIMD's oldest parser finishes first and its youngest
+            // runs on alone (stamps r06: 23 vs 41 us by age rank in one epoch launch)
+            const int lvl = rp_level(rp, rp.done_steps + g);
+            if (lvl != rp.prio) {
+                rp.prio = lvl;
+                set_prio_level(lvl);
+            }
             RP_STAMP(0);
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
