@@ -664,7 +664,9 @@ def main():
         "step_fp64_tflops": round(step_tf, 4),
         "step_fp64_frac": round(step_tf / FP64_PEAK_TFLOPS, 5),
         "consensus": {"kernel": "chunk_kernel", "ms": round(cavg, 4), "fp64_tflops": round(cons_tf, 4),
-                      "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "flops_per_launch": flops},
+                      "frac": round(cons_tf / FP64_PEAK_TFLOPS, 5), "flops_per_launch": flops,
+                      "not_in_kernel_ms": "cut_lane_kernel (the chunks' box terms and cutoffs, lane per chunk, "
+                                          "launched with seed_kernel on the seeding stream, DESIGN.md §4.2)"},
         "pipeline": {"ms": round(kavg, 4), "alg_bytes_per_launch": alg_bytes, "hbm_alg_gbs": round(hbm_gbs, 2),
                      "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 5)},
     })

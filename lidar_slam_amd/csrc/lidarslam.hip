@@ -163,6 +163,7 @@ struct KArgs {
     int32_t *cnt_scr;   // [n_chunks][T] inlier counts (= trial_cnt_out when given)
     double *models;     // [n_chunks][T][4] 2-point models (origin, direction)
     int cnt_blocks;     // count_kernel workgroups per chunk
+    const ChunkCut *cuts;  // chunk_kernel: [n_chunks] box terms and cutoffs from cut_lane_kernel (null: in-kernel)
     unsigned long long *dbg;  // diagnostic build only: [n_scans][8] cycle accumulators
     unsigned long long *wcen;  // diagnostic build only: wave census records [256][cap / 256][3] (WaveCensus)
     unsigned int *wcen_n;      // [256] records claimed so far per bucket
@@ -638,9 +639,8 @@ __device__ __forceinline__ cut_t cut_hi_of(double e) {
     return count_cut(sq_ceil_gt(e));
 }
 
-__device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecut_q) {
-    const int kxh = wave_max_dpp(b.xh), kxl = wave_max_dpp(~b.xl);  // keys of max x, -min x
-    const int kyh = wave_max_dpp(b.yh), kyl = wave_max_dpp(~b.yl);
+// from the four key maxima (x max, -x min, y max, -y min) of the chunk's points
+__device__ __forceinline__ ChunkCut cut_from_keys(int kxh, int kxl, int kyh, int kyl, double ecut, double ecut_q) {
     ChunkCut cc;
     cc.finite = key_finite(kxh) && key_finite(kxl) && key_finite(kyh) && key_finite(kyl);
     const double hx = key_up(kxh), lx = key_up(kxl), hy = key_up(kyh), ly = key_up(kyl);
@@ -665,15 +665,20 @@ __device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecu
     }
     return cc;
 }
+__device__ __forceinline__ ChunkCut cut_finish(BoxAcc b, double ecut, double ecut_q) {
+    return cut_from_keys(wave_max_dpp(b.xh), wave_max_dpp(~b.xl), wave_max_dpp(b.yh), wave_max_dpp(~b.yl), ecut,
+                         ecut_q);
+}
 
+// pcut: the chunk's box terms and cutoffs computed ahead (cut_lane_kernel), or null
 __device__ ChunkOut chunk_consensus(const KArgs &a, double2 *P, const double2 *gP, int N, const int32_t *draws,
                                     int32_t *cnt, int32_t *tied, double *tsum, uint8_t *mk, double *vtmp,
-                                    double *vstack, int *nstack, int32_t *cnt_out, int lane,
+                                    double *vstack, int *nstack, int32_t *cnt_out, int lane, const ChunkCut *pcut,
                                     unsigned long long *chdbg = nullptr) {
     CH_STAMP_DECL
     const int T = a.T;
     const double ecut = a.ecut;
-    const ChunkCut cc = chunk_cut(P, N, ecut, a.ecut_q, lane);
+    const ChunkCut cc = pcut ? *pcut : chunk_cut(P, N, ecut, a.ecut_q, lane);
     if (N > 128 || !cc.finite || !(ecut < __builtin_inf()))
         return chunk_ransac(a, P, N, draws, cnt, tied, tsum, mk, vstack, nstack, cnt_out, lane);
 
@@ -1867,6 +1872,29 @@ __global__ __launch_bounds__(64) void seed_kernel(const uint32_t *__restrict__ s
     }
 }
 
+// The chunks' box terms and cutoffs (chunk_cut) one lane per chunk, launched with seed_kernel on
+// the seeding stream beside the previous call (launch_seed), so the consensus on the context
+// stream -- the longer of the pipeline's two loops at r06 -- reads 32 bytes per
+// chunk instead of reducing its box over the wave (~220 of its ~3.3k instructions per chunk).
+// The same key maxima as cut_finish's DPP reduction, so the same ChunkCut.
+__global__ __launch_bounds__(64) void cut_lane_kernel(const KArgs a, ChunkCut *__restrict__ out) {
+    __builtin_amdgcn_s_setprio(2);
+    const lslam_scan_batch &B = a.b;
+    const int c = (int)blockIdx.x * 64 + (int)threadIdx.x;
+    if (c >= B.n_chunks) return;
+    const int p0 = B.chunk_pt_off[c];
+    const int N = B.chunk_pt_off[c + 1] - p0;
+    BoxAcc b;
+    if (B.xy) {
+        const double2 *src = (const double2 *)B.xy + p0;
+#pragma unroll 4
+        for (int p = 0; p < N; p++) b.add(src[p]);
+    } else {
+        for (int p = 0; p < N; p++) b.add(polar_xy(B.theta_deg[p0 + p], B.dist_mm[p0 + p]));
+    }
+    out[c] = cut_from_keys(b.xh, ~b.xl, b.yh, ~b.yl, a.ecut, a.ecut_q);
+}
+
 constexpr int RNG_PPW = 4;
 template <typename JT>
 __global__ __launch_bounds__(64 * RNG_PPW) void rng_kernel(const KArgs a) {
@@ -2520,7 +2548,8 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     CH_STAMP(6);
     const double2 *gP = B.xy ? (const double2 *)B.xy + p0 : nullptr;
     const ChunkOut o = chunk_consensus(a, P, gP, N, dr, cnt, tied, tsum, mk, vtmp, vstack, nstack,
-                                       B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane, chdbg);
+                                       B.trial_cnt_out ? B.trial_cnt_out + (size_t)c * T : nullptr, lane,
+                                       a.cuts ? a.cuts + c : nullptr, chdbg);
     CH_STAMP_DECL_RESET
     const bool have_model = finish_chunk(a, o, P, mk, p0, N, rec, lane);
     if (B.y_proj && a.write_yproj) chunk_yproj(B.y_proj + p0, P, mk, N, have_model, rec.proj_a, rec.proj_b, lane);
@@ -3011,6 +3040,13 @@ struct lslam_ctx {
     hipEvent_t ev_seeded[2];     // on sstream, after seed_kernel into seedst[i]
     hipEvent_t ev_seed_read[2];  // on pstream, after the producer that read seedst[i]
     int seed_next;               // the pipeline's next seed buffer
+    // cut_lane_kernel -> chunk_kernel: [n_chunks] ChunkCut, a ring of four by seeded call: the
+    // buffer of call n is written after the producer of seeded call n - 2 (ev_seed_read), which
+    // waited for its slot, released by the fix-up of the mt call two before it -- after the
+    // consensus of seeded call n - 4, the buffer's previous reader
+    ChunkCut *cutb[4];
+    size_t cutb_bytes[4];
+    int cut_next;
     size_t steps_budget;  // producer slot budget (prepare_steps)
     // The MT producer of call k+1 runs on its own stream while call k's
     // consumers finish on `stream`: two producer slots (Fisher-Yates steps +
@@ -3146,6 +3182,11 @@ int lslam_ctx_create(int device, lslam_ctx **out) {
     }
     c->sstream = nullptr;
     c->seed_next = 0;
+    for (int i = 0; i < 4; i++) {
+        c->cutb[i] = nullptr;
+        c->cutb_bytes[i] = 0;
+    }
+    c->cut_next = 0;
     c->escr = nullptr;
     c->escr_bytes = 0;
     c->cscr = nullptr;
@@ -3233,6 +3274,8 @@ int lslam_ctx_destroy(lslam_ctx *c) {
     if (c->scr) (void)hipFree(c->scr);
     for (int i = 0; i < 3; i++)
         if (c->seedst[i]) (void)hipFree(c->seedst[i]);
+    for (int i = 0; i < 4; i++)
+        if (c->cutb[i]) (void)hipFree(c->cutb[i]);
     for (int i = 0; i < 2; i++) {
         if (c->ev_seeded[i]) (void)hipEventDestroy(c->ev_seeded[i]);
         if (c->ev_seed_read[i]) (void)hipEventDestroy(c->ev_seed_read[i]);
@@ -3915,6 +3958,27 @@ static int launch_seed(lslam_ctx *c, KArgs &k, hipStream_t stream, bool on_side,
     hipLaunchKernelGGL(seed_kernel, dim3((unsigned)((k.b.n_scans + 63) / 64)), dim3(64), 0, ss, k.b.seeds,
                        (int)k.b.n_scans, c->seedst[i]);
     HIPCHK(hipGetLastError());
+    k.cuts = nullptr;
+    if (on_side && k.b.n_chunks > 0 && k.b.max_chunk_points <= 128) {  // chunk_kernel's chunks
+        const int j = c->cut_next;
+        const size_t cneed = (size_t)k.b.n_chunks * sizeof(ChunkCut);
+        if (c->cutb_bytes[j] < cneed) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(hipStreamSynchronize(c->pstream));
+            HIPCHK(hipStreamSynchronize(c->sstream));
+            if (c->cutb[j]) HIPCHK(hipFree(c->cutb[j]));
+            c->cutb[j] = nullptr;
+            c->cutb_bytes[j] = 0;
+            hipError_t e = hipMalloc(&c->cutb[j], cneed);
+            if (e == hipErrorOutOfMemory) return set_err(LSLAM_ERR_NOMEM, "hipMalloc: out of memory (chunk cutoffs)");
+            HIPCHK(e);
+            c->cutb_bytes[j] = cneed;
+        }
+        hipLaunchKernelGGL(cut_lane_kernel, dim3((unsigned)((k.b.n_chunks + 63) / 64)), dim3(64), 0, ss, k, c->cutb[j]);
+        HIPCHK(hipGetLastError());
+        k.cuts = c->cutb[j];
+        c->cut_next = (j + 1) & 3;
+    }
     if (on_side) {
         HIPCHK(hipEventRecord(c->ev_seeded[i], ss));
         HIPCHK(hipStreamWaitEvent(stream, c->ev_seeded[i], 0));

@@ -35,7 +35,8 @@ def counter(path, name, kernel_sub="scan_kernel"):
 
 # kernel-name substrings: producer, consensus, fix-up (scan_kernel<MT, RANSAC>), post pass (post_reg_kernel: the
 # association-only pass with the list in registers; scan_kernel<EXPLICIT, ...> for the other post modes)
-KERNELS = {"rng_kernel": "rng_kernel", "resolve_reg": "resolve_reg", "resolve_kernel": "resolve_kernel<",
+KERNELS = {"seed_kernel": "seed_kernel", "cut_lane_kernel": "cut_lane_kernel", "rng_kernel": "rng_kernel",
+           "resolve_reg": "resolve_reg", "resolve_kernel": "resolve_kernel<",
            "chunk_kernel": "chunk_kernel", "ukf_group_kernel": "ukf_group_kernel", "fixup": "scan_kernel<0, 1>",
            "post": "post_reg_kernel", "post_scan": "scan_kernel<2, "}
 

@@ -8,7 +8,7 @@ import csv
 import os
 import sys
 
-KERNELS = {"seed_kernel": "seed_kernel", "rng_kernel": "rng_kernel", "resolve_reg": "resolve_reg",
+KERNELS = {"seed_kernel": "seed_kernel", "cut_lane_kernel": "cut_lane_kernel", "rng_kernel": "rng_kernel", "resolve_reg": "resolve_reg",
            "chunk_kernel": "chunk_kernel", "ukf_group_kernel": "ukf_group_kernel", "fixup": "scan_kernel<0, 1>",
            "post": "post_reg_kernel"}
 KINDS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_INSTS_SMEM")
