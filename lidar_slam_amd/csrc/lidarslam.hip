@@ -110,7 +110,7 @@ struct ChunkCut {
     double margin;  // the exact-test band around ecut
     cut_t c_lo, c_hi;
     int finite;     // every point finite and the box bounds finite
-    int pad;
+    int scan;       // cut_lane_kernel: the chunk's owning scan (owning_scan), for chunk_kernel
 };
 
 // ------------------------------------------------------------------------
@@ -648,7 +648,7 @@ __device__ __forceinline__ ChunkCut cut_from_keys(int kxh, int kxl, int kyh, int
     const double E2 = (bx * bx + by * by) * (1.0 + 0x1p-20);
     const double Rb = (fmax(hx, lx) + fmax(hy, ly)) * (1.0 + 0x1p-40);  // >= max|x| + max|y|
     cc.finite = cc.finite && E2 < __builtin_inf();
-    cc.pad = 0;
+    cc.scan = 0;
     cc.tq = 0.0;
     cc.margin = 0.0;
     cc.c_lo = count_cut(-1.0);
@@ -1892,7 +1892,21 @@ __global__ __launch_bounds__(64) void cut_lane_kernel(const KArgs a, ChunkCut *_
     } else {
         for (int p = 0; p < N; p++) b.add(polar_xy(B.theta_deg[p0 + p], B.dist_mm[p0 + p]));
     }
-    out[c] = cut_from_keys(b.xh, ~b.xl, b.yh, ~b.yl, a.ecut, a.ecut_q);
+    ChunkCut cc = cut_from_keys(b.xh, ~b.xl, b.yh, ~b.yl, a.ecut, a.ecut_q);
+    // owning scan (owning_scan's guess and search, per lane): the consensus wave then skips its
+    // 64-bit division and dependent loads
+    int g = (int)(((int64_t)c * B.n_scans) / (B.n_chunks > 0 ? B.n_chunks : 1));
+    if (!(g < B.n_scans && B.scan_chunk_off[g] <= c && c < B.scan_chunk_off[g + 1])) {
+        int lo = 0, hi = B.n_scans;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (B.scan_chunk_off[mid] <= c) lo = mid;
+            else hi = mid;
+        }
+        g = lo;
+    }
+    cc.scan = g;
+    out[c] = cc;
 }
 
 constexpr int RNG_PPW = 4;
@@ -2491,7 +2505,7 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     int *nstack = (int *)(smem + a.off_nstack);
     double *vtmp = (double *)(smem + a.off_vtmp);
 
-    const int s = owning_scan(B, c);
+    const int s = a.cuts ? uni(a.cuts[c].scan) : owning_scan(B, c);
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
