@@ -185,7 +185,8 @@ typedef struct lslam_scan_batch {
     lslam_chunk_model *models;      /* [n_chunks] */
     double *y_proj;                 /* [n_points] projected y of inliers, 0 elsewhere (optional) */
     int32_t *draws_out;             /* [n_chunks][max_trials+1][2] (optional, parity/debug) */
-    int32_t *trial_cnt_out;         /* [n_chunks][max_trials] (optional, parity/debug) */
+    int32_t *trial_cnt_out;         /* [n_chunks][max_trials] (optional, parity/debug; zero rows
+                                       for chunks of fewer than 3 points) */
     /* UKF, per scan */
     double *ukf_x;                  /* [n_scans][3] in/out */
     double *ukf_P;                  /* [n_scans][3][3] in/out */

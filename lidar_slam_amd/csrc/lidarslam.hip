@@ -1537,6 +1537,8 @@ __device__ __forceinline__ void scan_body(const KArgs &a, const int s, unsigned 
                     if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
                     if (B.y_proj) B.y_proj[p0 + p] = 0.0;
                 }
+                if (B.trial_cnt_out)  // no trials: a zero row (lidarslam.h)
+                    for (int t = lane; t < a.T; t += 64) B.trial_cnt_out[(size_t)c * a.T + t] = 0;
                 __syncthreads();
                 continue;
             }
@@ -2528,6 +2530,8 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
             if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
             if (B.y_proj && a.write_yproj) B.y_proj[p0 + p] = 0.0;
         }
+        if (B.trial_cnt_out)  // no trials: a zero row (lidarslam.h)
+            for (int t = lane; t < a.T; t += 64) B.trial_cnt_out[(size_t)c * a.T + t] = 0;
         return;
     }
     const int D = T + 1;
@@ -2692,8 +2696,12 @@ __global__ __launch_bounds__(CNT_TPB) void count_kernel(const KArgs a) {
     const int p0 = B.chunk_pt_off[c];
     const int N = B.chunk_pt_off[c + 1] - p0;
     const int T = a.T;
-    if (N < 3 || t0 >= T) return;
+    if (t0 >= T) return;
     const int nt = min(CNT_HYP_BLOCK, T - t0);
+    if (N < 3) {  // no trials: a zero row (lidarslam.h)
+        for (int h = (int)threadIdx.x; h < nt; h += CNT_TPB) a.cnt_scr[(size_t)c * T + t0 + h] = 0;
+        return;
+    }
     for (int h = tid; h < nt; h += CNT_TPB) {
         s_lo[h] = 0;
         s_hi[h] = 0;
@@ -2854,6 +2862,8 @@ __global__ __launch_bounds__(64) void select_kernel(const KArgs a) {
             if (B.inlier_mask) B.inlier_mask[p0 + p] = 0;
             if (B.y_proj && a.write_yproj) B.y_proj[p0 + p] = 0.0;
         }
+        if (B.trial_cnt_out)  // no trials: a zero row (lidarslam.h)
+            for (int t = lane; t < a.T; t += 64) B.trial_cnt_out[(size_t)c * a.T + t] = 0;
         return;
     }
 #ifdef LSLAM_STAMPS
