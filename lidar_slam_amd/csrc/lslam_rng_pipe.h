@@ -271,9 +271,19 @@ __device__ __forceinline__ void parse_chunk(RngPipe &rp, int &blkno, int &pos, J
         }
         const uint32_t *kb = rp.blk + (blkno & 1) * MT_N;
         const uint32_t rem = G - g;
-        // a run of full windows: inside this block and short of the chunk's end
-        // (window r of the run still has > 64 steps left: r < (rem - 1) / 64)
-        const int nrun = FAST ? min((MT_N - pos) >> 6, (int)((rem - 1u) >> 6)) : 0;
+        // a run of full windows short of the chunk's end (window r of the run still has > 64 steps
+        // left: r < (rem - 1) / 64), up to and including the window across the block's end: as in
+        // table mode, the next block is twisted first and its words follow the block's in the LDS
+        // ([slot 0][slot 1][pad]), so a block's last words need no partial window (C5: one in
+        // eleven of its windows was the partial form, ~10 % of the producer)
+        // The next block is twisted when the parser enters a block (not when a run first crosses:
+        // a run cut short by the chunk's end prefetches the next run's first words, which may lie
+        // past the block's end, so those must already be the next block's).
+        if (FAST) {
+            rp_need_block(rp, blkno + 1, lane);
+            asm volatile("" ::: "memory");
+        }
+        const int nrun = FAST ? min((MT_N - pos + 63) >> 6, (int)((rem - 1u) >> 6)) : 0;
         if (nrun > 0) {
             uint32_t raw = (pre_pos == pos) ? pre_raw : kb[pos + lane];
             // software-pipelined temper: window r+1's words are tempered beside window r's fixed
