@@ -3902,13 +3902,15 @@ static int launch_resolve(lslam_ctx *c, const KArgs &base, hipStream_t rs) {
     k.res_g = lds;  // staging capacity in bytes
     if (lds == 0) {  // steps streamed from HBM, waves over (chunk, draw)
         const int64_t items = (int64_t)k.b.n_chunks * De;
-        // beside the next epoch's producer (produce_draws): three waves per SIMD beside its four
-        // parsers (r06, with the double-buffered walk: C5 65.7-66.1 vs 68.9-69.3 ms per call at
-        // two, 66.0-66.3 at four; the epoch loop is max(producer, resolve beside it), and at two
-        // the resolve was the longer).  (At r02, with five producer waves per SIMD, three
-        // displaced parser workgroups: 107 vs 78 ms.  Measured and dropped: LDS tiles of
-        // [64 draws][128 steps], 1.0 vs 0.43 ms per epoch.)
-        const int64_t cap = k.ep_count > 1 ? 12 * (int64_t)c->n_cus : (1 << 20);
+        // beside the next epoch's producer (produce_draws): four waves per SIMD beside its four
+        // parsers.  The epoch loop is max(producer, resolve beside it): with the double-buffered
+        // walk, three waves per SIMD measured 65.7-66.1 vs 68.9-69.3 ms per C5 call at two (r06d,
+        // four: 66.0-66.3); once mask-mode runs crossed block ends (r06f: a 9 % faster producer)
+        // the resolve was the longer again, and four gave 61.4-61.6 vs 63.5-63.6 ms at three.
+        // (At r02, with five producer waves per SIMD, three displaced parser workgroups: 107 vs
+        // 78 ms.  Measured and dropped: LDS tiles of [64 draws][128 steps], 1.0 vs 0.43 ms per
+        // epoch.)
+        const int64_t cap = k.ep_count > 1 ? 16 * (int64_t)c->n_cus : (1 << 20);
         const dim3 grid(launch_cap(c, items > cap ? cap : items)), block(64);
         if (k.j8) hipLaunchKernelGGL((resolve_walk_kernel<uint8_t, 16>), grid, block, 0, rs, k);
         else hipLaunchKernelGGL((resolve_walk_kernel<uint16_t, 16>), grid, block, 0, rs, k);
