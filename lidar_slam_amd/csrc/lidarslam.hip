@@ -2575,8 +2575,11 @@ __device__ __forceinline__ void chunk_body(const KArgs &a, const int c, unsigned
     CH_STAMP(5);
 }
 
+// At most 128 VGPRs (four waves per SIMD by registers): three consensus waves per SIMD then fit
+// beside the producer's four parsers.  An unbounded build drifted to 132 after an unrelated edit
+// and left two: consensus 0.382 vs 0.359 ms, step +3.4 % (r06g A/B).
 template <int HYP>
-__global__ __launch_bounds__(64) void chunk_kernel(const KArgs a) {
+__global__ __launch_bounds__(64, 4) void chunk_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     WAVE_CENSUS(a, WC_CHUNK);
     for (int c = blockIdx.x; c < a.b.n_chunks; c += gridDim.x) {
